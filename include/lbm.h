@@ -1,0 +1,143 @@
+/*
+ * lbm.h -- C ABI of liblbm.so, the MI355X-native D3Q19 BGK collide+stream hot path.
+ *
+ * This is the drop-in boundary for the reference's per-case kernel-launch interface.
+ * The reference has no library API: each case's main() launches, per time step,
+ *
+ *   update<<<>>>(NLATTICE, d_geo, d_scr, d_dst, d_ux, d_uy, d_uz, d_rho, tau)
+ *                          ldc.cu:57, Poiseulle.cu:384 (geo/index via textures 49-50),
+ *                          bifurcation.cu:429 (tau hard-coded 434)
+ *   boundary_stream<<<>>>(NLATTICE, d_geo, d_dst, d_ux, d_uy, d_uz, d_rho, tau, C_U)
+ *                          ldc.cu:373, Poiseulle.cu:585, bifurcation.cu:639
+ *   calc_vel_square<<<>>>(d_velsum, d_ux, d_uy, d_uz, NLATTICE) + thrust::reduce
+ *                          ldc.cu:460-466,660-662, Poiseulle.cu:895-901,993-996
+ *   d_scr <-> d_dst pointer swap
+ *                          ldc.cu:664-666
+ *
+ * and owns the buffers itself (cudaMalloc/cudaMemcpy in main, ldc.cu:635-650).  Here
+ * one opaque context owns the device buffers of one lattice (or one z-slab of it),
+ * and lbm_step() performs all of the above for n steps: a fused pull-stream +
+ * collide kernel with wall bounce-back and non-equilibrium-extrapolation
+ * boundaries evaluated by mask on the consumer side, a fused |u| reduction, a
+ * device-side residual/convergence finisher, and (for slabs) the +-z halo exchange
+ * over RCCL.  All pointers in these signatures are plain host pointers; no HIP or
+ * torch types cross the boundary.  Every function returns LBM_OK (0) or a negative
+ * status; lbm_last_error() gives the message.  One context per host thread at a
+ * time; contexts are not re-entrant.
+ */
+#ifndef LBM_H
+#define LBM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBM_OK 0
+#define LBM_ERR_ARG -1
+#define LBM_ERR_HIP -2
+#define LBM_ERR_RCCL -3
+#define LBM_ERR_STATE -4
+#define LBM_ERR_GEOMETRY -5
+
+/* Which reference case supplies the meaning of the mask codes (README.md:9-14). */
+typedef enum {
+  LBM_CASE_LDC = 0,        /* ldc.cu: 0 ghost, 1 wall (bounce-back already at step 0),
+                              2 moving lid (velocity NEE, -y face), 3 fluid */
+  LBM_CASE_POISEUILLE = 1, /* Poiseulle.cu: -1 ghost, 0 unused, 1 wall, 2 inlet (velocity NEE,
+                              +y face), 3 outlet (velocity NEE, -y face), 4 fluid */
+  LBM_CASE_MASK = 2        /* bifurcation.cu: as Poiseuille but 3 = pressure outlet (rho = 1,
+                              u = u of the fluid neighbour) */
+} lbm_case_kind;
+
+/* Equilibrium expression used to initialise f (the two forms of the reference). */
+typedef enum {
+  LBM_INIT_LDC_WI = 0,     /* ldc.cu:553-571: rho*w_q*(1 + 3 e.u + 4.5 (e.u)^2 - 1.5 u^2) */
+  LBM_INIT_EXPANDED = 1    /* Poiseulle.cu:354-372 / bifurcation.cu:399-417: update-kernel form */
+} lbm_init_form;
+
+typedef struct lbm_ctx lbm_ctx;
+
+typedef struct {
+  int nx, ny, nz;          /* extent of this context's lattice (its slab when nz_global > nz) */
+  float tau;               /* BGK relaxation time (ldc.cu:55, Poiseulle.cu:39, bifurcation.cu:434) */
+  int case_kind;           /* lbm_case_kind */
+  /* Reference mask codes, raster x fastest then y then z (int8).  Planes: nz, or nz + 2 when
+   * halo_planes = 1 (plane 0 = global z_offset-1, plane nz+1 = global z_offset+nz).  NULL with
+   * LBM_CASE_LDC: the cavity box of ldc.cu:468-502 is generated on the device from global
+   * coordinates (used for the multi-GB benchmark lattices). */
+  const int8_t* geo;
+  int halo_planes;
+  float lid_u;             /* LDC lid speed along +z (ldc.cu:52: 0.15f / C_U) */
+  const float* bc_inlet_uy;  /* nx * nz_global floats, x fastest: u_y imposed on code-2 cells (nullable) */
+  const float* bc_outlet_uy; /* nx * nz_global floats: u_y on code-3 cells (LBM_CASE_POISEUILLE) */
+  int device;              /* HIP device ordinal */
+  int z_offset;            /* global z of local plane 0 */
+  int nz_global;           /* global z extent (== nz for a single-domain run) */
+} lbm_desc;
+
+/* Status / version */
+const char* lbm_version(void);
+const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error */
+
+/* Lifecycle */
+int lbm_create(const lbm_desc* desc, lbm_ctx** out);
+void lbm_destroy(lbm_ctx* ctx);
+
+/* Initial state.  rho/ux/uy/uz are nx*ny*nz raster arrays (nullable: rho=1, u=0); the
+ * equilibrium is evaluated on the device with the chosen reference expression into both
+ * population buffers, bit-identical to the reference initialize(). */
+int lbm_init_equilibrium(lbm_ctx* ctx, int form, const float* rho, const float* ux,
+                         const float* uy, const float* uz);
+/* LDC initial state of ldc.cu:504-580 generated on the device (no host arrays). */
+int lbm_init_ldc(lbm_ctx* ctx);
+/* Exact initial populations, SoA [19][nz][ny][nx] (into both buffers); resets the step count. */
+int lbm_set_f(lbm_ctx* ctx, const float* f_soa);
+
+/* Convergence control of the reference main loop (ldc.cu:653-685): when enabled, a device
+ * flag stops stepping once !(k <= max_it && tol_count <= stag_max); further steps are no-ops. */
+int lbm_set_convergence(lbm_ctx* ctx, int enabled, int max_it, int stag_max, float tol);
+
+/* Run n steps.  residual_hist (nullable, n floats) receives |S_k - S_{k-1}| / S_k per step,
+ * S = sum over cells of |u| (ldc.cu:660-668); when it is non-NULL, or steps_done is non-NULL,
+ * the call synchronises.  Otherwise the work is only enqueued (see lbm_sync). */
+int lbm_step(lbm_ctx* ctx, int nsteps, float* residual_hist, int* steps_done);
+int lbm_sync(lbm_ctx* ctx);
+
+/* Convergence state: k (steps executed), tol_count, stopped flag, last residual, last S. */
+int lbm_get_state(lbm_ctx* ctx, int* k, int* tol_count, int* stopped, float* residual, double* velsum);
+
+/* Macroscopic fields of the last step, raster nx*ny*nz; 0 off-fluid (nullable outputs). */
+int lbm_get_macros(lbm_ctx* ctx, float* rho, float* ux, float* uy, float* uz);
+/* Populations of the last step (the next step's source), SoA [19][nz][ny][nx]; only fluid
+ * cells carry reference-defined values. */
+int lbm_get_f(lbm_ctx* ctx, float* f_soa);
+
+/* Sizes: cells in the box, fluid cells, and the bytes one step moves algorithmically
+ * (152 B per fluid cell: 19 fp32 loads + 19 fp32 stores). */
+int lbm_get_counts(lbm_ctx* ctx, int64_t* n_box, int64_t* n_fluid, double* algo_bytes_per_step);
+
+/* Kernel timing: when enabled, HIP events bracket every collide-stream launch on the
+ * stream it runs on; lbm_stats returns the summed kernel milliseconds and launch count
+ * since enabling. */
+int lbm_profile(lbm_ctx* ctx, int enabled);
+int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
+
+/* Multi-GPU z-slabs (one process per GPU).  Rank 0 calls lbm_rccl_unique_id, the 128 bytes
+ * are broadcast by the caller (e.g. torch.distributed), then every rank attaches.  After
+ * attaching, lbm_step exchanges the 5 populations crossing each +-z face every step over
+ * RCCL on a communication stream, overlapped with the interior update, and all-reduces the
+ * residual sum. */
+int lbm_rccl_unique_id(uint8_t out_id[128]);
+int lbm_attach_rccl(lbm_ctx* ctx, const uint8_t id[128], int rank, int nranks);
+
+/* Single-device loopback decomposition (test and debug path): n contexts, each a z-slab of
+ * one lattice on the same device, stepped together with device-to-device halo copies. */
+int lbm_group_step(lbm_ctx** ctxs, int n, int nsteps, float* residual_hist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LBM_H */

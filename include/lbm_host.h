@@ -1,0 +1,52 @@
+/*
+ * lbm_host.h -- C ABI of liblbm_host.so: the host side of the per-case API that the
+ * reference keeps inside each case's .cu file (geometry ingest, boundary tables,
+ * initial fields and output).  Plain C++, no device code; used by the case drivers
+ * (the drivers in lattice-boltzmann-method-gpu_amd/host) and by the Python bindings.
+ *
+ * All arrays are raster, x fastest, then y, then z ("[nz][ny][nx]").  Boundary tables
+ * are [nz][nx].
+ */
+#ifndef LBM_HOST_H
+#define LBM_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* geo_pre of the three cases: reference mask codes (README.md:9-14) */
+void lbmh_geo_ldc(int nx, int ny, int nz, int8_t* geo);                      /* ldc.cu:468-502 */
+void lbmh_geo_poiseuille(int nx, int ny, int nz, int8_t* geo);               /* Poiseulle.cu:52-255 */
+void lbmh_geo_mask(int nx, int ny, int nz, const int32_t* raw, int8_t* geo); /* bifurcation.cu:63-239 */
+/* geo.txt: nx*ny*nz whitespace-separated ints, z, y, x loop order (bifurcation.cu:50-60).
+ * Returns the number of ints read (< 0: cannot open). */
+long lbmh_read_geo_txt(const char* path, int nx, int ny, int nz, int32_t* raw);
+/* bc.txt (bifurcation.cu:294-325): block `inlet_block` is read as the inlet u_y on code-2 cells
+ * of the y=1 plane, the next block as the outlet u_y on code-3 cells of y=ny-2 (inlet_block = 0
+ * reproduces the shipped code; 1 reads the block that matches the shipped inlet).  Returns the
+ * number of tokens consumed (< 0: cannot open). */
+long lbmh_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* geo, int inlet_block,
+                      float* inlet_uy, float* outlet_uy);
+/* index_transform (Poiseulle.cu:257-271): compact ids in z,y,x order over geo != 0 (else -1).
+ * Returns NLATTICE. */
+int64_t lbmh_index_transform(int nx, int ny, int nz, const int8_t* geo, int32_t* index);
+/* the Poiseuille kernel's parabola uygt(x, z) (Poiseulle.cu:590,597) as a [nz][nx] table */
+void lbmh_poiseuille_profile(int nx, int nz, float u_max, float* table);
+/* initial (rho, u) of initialize(): case 0 LDC (ldc.cu:510-532), 1 Poiseuille
+ * (Poiseulle.cu:280-341, host u_max = 0.15f/C_U), 2 mask (bifurcation.cu:333-373) */
+void lbmh_initial_fields(int case_kind, int nx, int ny, int nz, const int8_t* geo, const float* inlet_uy,
+                         const float* outlet_uy, float* rho, float* ux, float* uy, float* uz);
+/* outputSave (legacy ASCII VTK of u*C_U): ldc.cu:582-610 (case 0), Poiseulle.cu:903-938 (1),
+ * bifurcation.cu:1095-1156 (2).  Returns 0 or < 0 when the file cannot be written. */
+int lbmh_write_vtk(const char* path, int case_kind, int nx, int ny, int nz, const int8_t* geo,
+                   const float* ux, const float* uy, const float* uz, float C_U, float CH);
+/* calc_res (bifurcation.cu:1158-1175): sum of |u|^2 over code >= 4 in the output region */
+double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
+                     const float* uz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LBM_HOST_H */

@@ -1,0 +1,388 @@
+"""lbm_amd -- Python bindings of liblbm.so (the HIP D3Q19 hot path) and liblbm_host.so
+(the per-case host ingest/output), used by tests/, bench.py and __graft_entry__.py.
+
+The product is the C ABI declared in include/lbm.h and include/lbm_host.h; this module
+only marshals numpy arrays through ctypes.  There is no CPU fallback: every solver
+call goes to liblbm.so, and a missing library or device raises.
+
+torch is imported before liblbm.so is loaded so that both share one HIP runtime (the
+wheel bundles its own libamdhip64.so.7/librccl.so.1; liblbm.so's DT_NEEDED sonames
+then resolve to those copies instead of loading a second runtime).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+try:  # shared HIP runtime (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is always present in this image
+    torch = None
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)                      # lattice-boltzmann-method-gpu_amd/
+LIB = os.path.join(ROOT, "lib")
+LIBLBM = os.path.join(LIB, "liblbm.so")
+LIBHOST = os.path.join(LIB, "liblbm_host.so")
+
+LBM_CASE_LDC, LBM_CASE_POISEUILLE, LBM_CASE_MASK = 0, 1, 2
+LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
+
+# reference per-case constants
+LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55
+POIS_TAU, POIS_C_U, POIS_UMAX_KERNEL = 0.58, 1.5441, 0.09714700668       # Poiseulle.cu:39,590
+BIF_TAU, BIF_C_U, BIF_CH = 0.55, 0.24159041, 0.000248925                 # bifurcation.cu:20,434
+BIF_SHAPE = (32, 83, 64)                                                 # (nz, ny, nx)
+
+
+def lid_u() -> float:
+    """u_max = 0.15f / C_U of ldc.cu:52, rounded in fp32 like the reference."""
+    return float(np.float32(0.15) / np.float32(LDC_C_U))
+
+
+class LbmError(RuntimeError):
+    pass
+
+
+class lbm_desc(C.Structure):
+    _fields_ = [
+        ("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int),
+        ("tau", C.c_float),
+        ("case_kind", C.c_int),
+        ("geo", C.POINTER(C.c_int8)),
+        ("halo_planes", C.c_int),
+        ("lid_u", C.c_float),
+        ("bc_inlet_uy", C.POINTER(C.c_float)),
+        ("bc_outlet_uy", C.POINTER(C.c_float)),
+        ("device", C.c_int),
+        ("z_offset", C.c_int),
+        ("nz_global", C.c_int),
+    ]
+
+
+# every symbol include/lbm.h and include/lbm_host.h declare (checked by the CPU tests)
+LBM_SYMBOLS = [
+    "lbm_version", "lbm_last_error", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
+    "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
+    "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
+]
+HOST_SYMBOLS = [
+    "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
+    "lbmh_index_transform", "lbmh_poiseuille_profile", "lbmh_initial_fields", "lbmh_write_vtk", "lbmh_calc_res",
+]
+
+_lbm = None
+_host = None
+
+i8p = C.POINTER(C.c_int8)
+i32p = C.POINTER(C.c_int32)
+f32p = C.POINTER(C.c_float)
+f64p = C.POINTER(C.c_double)
+i64p = C.POINTER(C.c_int64)
+ip = C.POINTER(C.c_int)
+P = C.c_void_p
+
+
+def _ptr(a: np.ndarray | None, ct):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def host_lib() -> C.CDLL:
+    global _host
+    if _host is None:
+        if not os.path.exists(LIBHOST):
+            raise LbmError(f"{LIBHOST} missing: run `make -C {ROOT}` or __graft_entry__.build()")
+        L = C.CDLL(LIBHOST)
+        sig = {
+            "lbmh_geo_ldc": (None, [C.c_int, C.c_int, C.c_int, i8p]),
+            "lbmh_geo_poiseuille": (None, [C.c_int, C.c_int, C.c_int, i8p]),
+            "lbmh_geo_mask": (None, [C.c_int, C.c_int, C.c_int, i32p, i8p]),
+            "lbmh_read_geo_txt": (C.c_long, [C.c_char_p, C.c_int, C.c_int, C.c_int, i32p]),
+            "lbmh_read_bc_txt": (C.c_long, [C.c_char_p, C.c_int, C.c_int, C.c_int, i8p, C.c_int, f32p, f32p]),
+            "lbmh_index_transform": (C.c_int64, [C.c_int, C.c_int, C.c_int, i8p, i32p]),
+            "lbmh_poiseuille_profile": (None, [C.c_int, C.c_int, C.c_float, f32p]),
+            "lbmh_initial_fields": (None, [C.c_int, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p, f32p, f32p, f32p]),
+            "lbmh_write_vtk": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p,
+                                         C.c_float, C.c_float]),
+            "lbmh_calc_res": (C.c_double, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        _host = L
+    return _host
+
+
+def lbm_lib() -> C.CDLL:
+    global _lbm
+    if _lbm is None:
+        if not os.path.exists(LIBLBM):
+            raise LbmError(f"{LIBLBM} missing: run `make -C {ROOT}` or __graft_entry__.build()")
+        L = C.CDLL(LIBLBM)
+        sig = {
+            "lbm_version": (C.c_char_p, []),
+            "lbm_last_error": (C.c_char_p, [P]),
+            "lbm_create": (C.c_int, [C.POINTER(lbm_desc), C.POINTER(P)]),
+            "lbm_destroy": (None, [P]),
+            "lbm_init_equilibrium": (C.c_int, [P, C.c_int, f32p, f32p, f32p, f32p]),
+            "lbm_init_ldc": (C.c_int, [P]),
+            "lbm_set_f": (C.c_int, [P, f32p]),
+            "lbm_set_convergence": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_float]),
+            "lbm_step": (C.c_int, [P, C.c_int, f32p, ip]),
+            "lbm_sync": (C.c_int, [P]),
+            "lbm_get_state": (C.c_int, [P, ip, ip, ip, f32p, f64p]),
+            "lbm_get_macros": (C.c_int, [P, f32p, f32p, f32p, f32p]),
+            "lbm_get_f": (C.c_int, [P, f32p]),
+            "lbm_get_counts": (C.c_int, [P, i64p, i64p, f64p]),
+            "lbm_profile": (C.c_int, [P, C.c_int]),
+            "lbm_stats": (C.c_int, [P, f64p, i64p, f64p]),
+            "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+            "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+            "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        _lbm = L
+    return _lbm
+
+
+def version() -> str:
+    return lbm_lib().lbm_version().decode()
+
+
+# ---------------------------------------------------------------------------------------
+# host ingest (liblbm_host.so)
+# ---------------------------------------------------------------------------------------
+
+def geo_ldc(nx: int, ny: int, nz: int) -> np.ndarray:
+    g = np.zeros((nz, ny, nx), np.int8)
+    host_lib().lbmh_geo_ldc(nx, ny, nz, _ptr(g, C.c_int8))
+    return g
+
+
+def geo_poiseuille(nx: int, ny: int, nz: int) -> np.ndarray:
+    g = np.zeros((nz, ny, nx), np.int8)
+    host_lib().lbmh_geo_poiseuille(nx, ny, nz, _ptr(g, C.c_int8))
+    return g
+
+
+def read_geo_txt(path: str, shape=BIF_SHAPE) -> np.ndarray:
+    nz, ny, nx = shape
+    raw = np.zeros(shape, np.int32)
+    n = host_lib().lbmh_read_geo_txt(path.encode(), nx, ny, nz, _ptr(raw, C.c_int32))
+    if n != raw.size:
+        raise LbmError(f"{path}: read {n} of {raw.size} mask values")
+    return raw
+
+
+def geo_mask(raw: np.ndarray) -> np.ndarray:
+    raw = np.ascontiguousarray(raw, np.int32)
+    nz, ny, nx = raw.shape
+    g = np.zeros(raw.shape, np.int8)
+    host_lib().lbmh_geo_mask(nx, ny, nz, _ptr(raw, C.c_int32), _ptr(g, C.c_int8))
+    return g
+
+
+def read_bc_txt(path: str, geo: np.ndarray, inlet_block: int = 0):
+    nz, ny, nx = geo.shape
+    inl = np.zeros((nz, nx), np.float32)
+    out = np.zeros((nz, nx), np.float32)
+    n = host_lib().lbmh_read_bc_txt(path.encode(), nx, ny, nz, _ptr(np.ascontiguousarray(geo), C.c_int8),
+                                    inlet_block, _ptr(inl, C.c_float), _ptr(out, C.c_float))
+    if n < 0:
+        raise LbmError(f"cannot read {path}")
+    return int(n), inl, out
+
+
+def index_transform(geo: np.ndarray):
+    g = np.ascontiguousarray(geo, np.int8)
+    nz, ny, nx = g.shape
+    idx = np.zeros(g.shape, np.int32)
+    n = host_lib().lbmh_index_transform(nx, ny, nz, _ptr(g, C.c_int8), _ptr(idx, C.c_int32))
+    return int(n), idx
+
+
+def poiseuille_profile(nx: int, nz: int, u_max: float = POIS_UMAX_KERNEL) -> np.ndarray:
+    t = np.zeros((nz, nx), np.float32)
+    host_lib().lbmh_poiseuille_profile(nx, nz, u_max, _ptr(t, C.c_float))
+    return t
+
+
+def initial_fields(case_kind: int, geo: np.ndarray, inlet_uy=None, outlet_uy=None):
+    g = np.ascontiguousarray(geo, np.int8)
+    nz, ny, nx = g.shape
+    out = [np.zeros(g.shape, np.float32) for _ in range(4)]
+    inl = None if inlet_uy is None else np.ascontiguousarray(inlet_uy, np.float32)
+    outl = None if outlet_uy is None else np.ascontiguousarray(outlet_uy, np.float32)
+    host_lib().lbmh_initial_fields(case_kind, nx, ny, nz, _ptr(g, C.c_int8), _ptr(inl, C.c_float),
+                                   _ptr(outl, C.c_float), *[_ptr(a, C.c_float) for a in out])
+    return tuple(out)
+
+
+def write_vtk(path: str, case_kind: int, geo: np.ndarray, ux, uy, uz, C_U: float, CH: float) -> None:
+    g = np.ascontiguousarray(geo, np.int8)
+    nz, ny, nx = g.shape
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (ux, uy, uz)]
+    rc = host_lib().lbmh_write_vtk(path.encode(), case_kind, nx, ny, nz, _ptr(g, C.c_int8),
+                                   *[_ptr(a, C.c_float) for a in arrs], C_U, CH)
+    if rc != 0:
+        raise LbmError(f"cannot write {path}")
+
+
+def calc_res(geo: np.ndarray, ux, uy, uz) -> float:
+    g = np.ascontiguousarray(geo, np.int8)
+    nz, ny, nx = g.shape
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (ux, uy, uz)]
+    return float(host_lib().lbmh_calc_res(nx, ny, nz, _ptr(g, C.c_int8), *[_ptr(a, C.c_float) for a in arrs]))
+
+
+# ---------------------------------------------------------------------------------------
+# solver contexts (liblbm.so)
+# ---------------------------------------------------------------------------------------
+
+class Lattice:
+    """One liblbm context: a lattice, or one z-slab of it, on one GPU."""
+
+    def __init__(self, case_kind: int, shape, tau: float, geo: np.ndarray | None = None, *,
+                 halo_planes: bool = False, lid_u_val: float | None = None, inlet_uy=None, outlet_uy=None,
+                 device: int = 0, z_offset: int = 0, nz_global: int | None = None):
+        nz, ny, nx = shape
+        self.shape = (nz, ny, nx)
+        self.case_kind = case_kind
+        d = lbm_desc()
+        d.nx, d.ny, d.nz = nx, ny, nz
+        d.tau = tau
+        d.case_kind = case_kind
+        self._keep = []
+        if geo is not None:
+            g = np.ascontiguousarray(geo, np.int8)
+            want = (nz + 2 if halo_planes else nz, ny, nx)
+            if g.shape != want:
+                raise LbmError(f"geo shape {g.shape} != {want}")
+            self._keep.append(g)
+            d.geo = _ptr(g, C.c_int8)
+        d.halo_planes = 1 if halo_planes else 0
+        d.lid_u = lid_u() if lid_u_val is None else lid_u_val
+        for name, tab in (("bc_inlet_uy", inlet_uy), ("bc_outlet_uy", outlet_uy)):
+            if tab is not None:
+                t = np.ascontiguousarray(tab, np.float32)
+                self._keep.append(t)
+                setattr(d, name, _ptr(t, C.c_float))
+        d.device = device
+        d.z_offset = z_offset
+        d.nz_global = nz if nz_global is None else nz_global
+        self.desc = d
+        h = P()
+        rc = lbm_lib().lbm_create(C.byref(d), C.byref(h))
+        if rc != 0:
+            raise LbmError(f"lbm_create: {lbm_lib().lbm_last_error(None).decode()}")
+        self.h = h
+
+    def _ck(self, rc: int, what: str):
+        if rc != 0:
+            raise LbmError(f"{what}: {lbm_lib().lbm_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lbm_lib().lbm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def init_equilibrium(self, form: int, rho=None, ux=None, uy=None, uz=None):
+        arrs = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (rho, ux, uy, uz)]
+        self._ck(lbm_lib().lbm_init_equilibrium(self.h, form, *[_ptr(a, C.c_float) for a in arrs]),
+                 "lbm_init_equilibrium")
+
+    def init_ldc(self):
+        self._ck(lbm_lib().lbm_init_ldc(self.h), "lbm_init_ldc")
+
+    def set_f(self, f: np.ndarray):
+        a = np.ascontiguousarray(f, np.float32)
+        self._ck(lbm_lib().lbm_set_f(self.h, _ptr(a, C.c_float)), "lbm_set_f")
+
+    def set_convergence(self, enabled=True, max_it=10000, stag_max=50, tol=1e-6):
+        self._ck(lbm_lib().lbm_set_convergence(self.h, 1 if enabled else 0, max_it, stag_max, tol),
+                 "lbm_set_convergence")
+
+    def step(self, n: int, history: bool = True):
+        if not history:
+            self._ck(lbm_lib().lbm_step(self.h, n, None, None), "lbm_step")
+            return None
+        hist = np.zeros(max(n, 1), np.float32)
+        done = C.c_int(0)
+        self._ck(lbm_lib().lbm_step(self.h, n, _ptr(hist, C.c_float), C.byref(done)), "lbm_step")
+        return hist[:n]
+
+    def sync(self):
+        self._ck(lbm_lib().lbm_sync(self.h), "lbm_sync")
+
+    def state(self):
+        k, tc, st = C.c_int(), C.c_int(), C.c_int()
+        r, s = C.c_float(), C.c_double()
+        self._ck(lbm_lib().lbm_get_state(self.h, C.byref(k), C.byref(tc), C.byref(st), C.byref(r), C.byref(s)),
+                 "lbm_get_state")
+        return {"k": k.value, "tol_count": tc.value, "stopped": bool(st.value), "residual": r.value,
+                "velsum": s.value}
+
+    def macros(self):
+        out = [np.zeros(self.shape, np.float32) for _ in range(4)]
+        self._ck(lbm_lib().lbm_get_macros(self.h, *[_ptr(a, C.c_float) for a in out]), "lbm_get_macros")
+        return tuple(out)
+
+    def f(self) -> np.ndarray:
+        a = np.zeros((19,) + self.shape, np.float32)
+        self._ck(lbm_lib().lbm_get_f(self.h, _ptr(a, C.c_float)), "lbm_get_f")
+        return a
+
+    def counts(self):
+        nb, nf, by = C.c_int64(), C.c_int64(), C.c_double()
+        self._ck(lbm_lib().lbm_get_counts(self.h, C.byref(nb), C.byref(nf), C.byref(by)), "lbm_get_counts")
+        return {"n_box": nb.value, "n_fluid": nf.value, "algo_bytes_per_step": by.value}
+
+    def profile(self, enabled: bool = True):
+        self._ck(lbm_lib().lbm_profile(self.h, 1 if enabled else 0), "lbm_profile")
+
+    def stats(self):
+        ms, n, by = C.c_double(), C.c_int64(), C.c_double()
+        self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
+        return {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
+
+    def attach_rccl(self, uid: bytes, rank: int, nranks: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._ck(lbm_lib().lbm_attach_rccl(self.h, buf, rank, nranks), "lbm_attach_rccl")
+
+
+def rccl_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    rc = lbm_lib().lbm_rccl_unique_id(buf)
+    if rc != 0:
+        raise LbmError(f"lbm_rccl_unique_id: {lbm_lib().lbm_last_error(None).decode()}")
+    return bytes(buf)
+
+
+def group_step(lats, n: int, history: bool = True):
+    arr = (P * len(lats))(*[l.h for l in lats])
+    hist = np.zeros(max(n, 1), np.float32) if history else None
+    rc = lbm_lib().lbm_group_step(arr, len(lats), n, _ptr(hist, C.c_float))
+    if rc != 0:
+        raise LbmError(f"lbm_group_step: {lbm_lib().lbm_last_error(lats[0].h).decode()}")
+    return None if hist is None else hist[:n]
+
+
+def gpu_available() -> bool:
+    return torch is not None and torch.cuda.is_available()
+
+
+def require_gpu():
+    if not gpu_available():
+        raise LbmError("no HIP device visible: liblbm.so has no CPU fallback")

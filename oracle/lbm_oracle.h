@@ -1,0 +1,85 @@
+/*
+ * lbm_oracle.h -- CPU restatement of the reference D3Q19 BGK hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (liblbm.so, liblbm_host.so,
+ * the case drivers) links, includes or calls this code.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only
+ * as the checker / the timed serial CPU baseline.
+ *
+ * It restates, in plain serial C, the algorithm of
+ *   /root/reference/Lid_driven_cavity/ldc.cu     (update 57-371, boundary_stream 373-458,
+ *                                                  geo_pre 468-502, initialize 504-580)
+ *   /root/reference/Poiseulle_flow/Poiseulle.cu  (geo_pre 52-255, index_transform 257-271,
+ *                                                  initialize 273-382, update 384-583,
+ *                                                  boundary_stream 585-893)
+ *   /root/reference/bifurcation/bifurcation.cu   (geo_pre 36-253, read_vel 255-327,
+ *                                                  initialize 329-427, update 429-637,
+ *                                                  boundary_stream 639-1023, calc_res 1158-1175)
+ * keeping the reference's two-pass structure (collide+pull pass, then a separate
+ * boundary pass that writes bounce-back and non-equilibrium-extrapolation values
+ * into boundary cells), its expression trees, and its fp32 evaluation order.
+ * Build with -ffp-contract=off (see oracle/Makefile).
+ *
+ * Pinning: see oracle/PINNING.md.  The reference is CUDA-only and cannot be
+ * built in this image (no nvcc; hipcc rejects <direct.h> and texture refs), so
+ * field-level parity against a reference binary is UNPINNED; the oracle is pinned
+ * by the reference's own known answers (thesis NLATTICE 65820, the shipped
+ * geo.txt/bc.txt), by analytic Poiseuille flow, and cross-checked against the
+ * emulation-probe numbers recorded in SURVEY.md.
+ *
+ * Storage: raster x-fastest, c = x + nx*(y + ny*z); populations SoA f[q*ncell + c].
+ */
+#ifndef LBM_ORACLE_H
+#define LBM_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_LDC = 0, ORC_POISEUILLE = 1, ORC_MASK = 2 };
+/* LDC wall bounce-back ordering: the reference (ldc.cu:184-201 vs 204-313) races. */
+enum { ORC_LDC_TWO_PHASE = 0,   /* all wall writes before any fluid read (race-free) */
+       ORC_LDC_SERIAL_EMU = 1 }; /* serial emulation order: blocks z,y,x; threads y,x; koff 7..0 */
+
+typedef struct orc_lbm orc_lbm;
+
+/* ---- geometry builders (reference geo_pre), raster int8 reference codes ---- */
+void orc_geo_ldc(int nx, int ny, int nz, int8_t* geo);                      /* ldc.cu:468-502 */
+void orc_geo_poiseuille(int nx, int ny, int nz, int8_t* geo);               /* Poiseulle.cu:52-255 */
+void orc_geo_mask(int nx, int ny, int nz, const int32_t* raw, int8_t* geo); /* bifurcation.cu:36-253 */
+int  orc_read_geo_txt(const char* path, int n, int32_t* raw);               /* bifurcation.cu:50-60 */
+/* bifurcation.cu:255-327: fills inlet (y=1, geo==2) and outlet (y=ny-2, geo==3) uy tables,
+ * skipping `skip_blocks` nx*nz blocks first (1 = the "inlet = block 1" variant). Returns tokens read. */
+int  orc_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* geo, int skip_blocks,
+                     float* inlet_uy, float* outlet_uy);
+/* Poiseulle.cu:257-271: compact ids in z,y,x raster over geo != 0. Returns NLATTICE. */
+int  orc_index_transform(int nx, int ny, int nz, const int8_t* geo, int32_t* index);
+
+/* ---- solver ---- */
+orc_lbm* orc_create(int case_kind, int nx, int ny, int nz, const int8_t* geo, float tau,
+                    int ldc_order, const float* inlet_uy, const float* outlet_uy);
+void orc_destroy(orc_lbm* o);
+/* reference initialize(): LDC wi-form (ldc.cu:504-580) / expanded form (Poiseulle.cu:273-382,
+ * bifurcation.cu:329-427), with each case's initial rho/u rules. */
+void orc_initialize(orc_lbm* o);
+/* Run n steps; residual_hist (nullable, n floats) gets the reference residual of each step. */
+void orc_step(orc_lbm* o, int n, float* residual_hist);
+/* Run the reference convergence loop (ldc.cu:653-685): returns final k. */
+int  orc_run_converge(orc_lbm* o, int max_it, int stag_max, float tol, float* last_residual);
+int  orc_steps_done(const orc_lbm* o);
+/* raster copies; macros are the last step's d_rho/d_ux/d_uy/d_uz (0 where never written) */
+void orc_get_macros(const orc_lbm* o, float* rho, float* ux, float* uy, float* uz);
+void orc_get_f(const orc_lbm* o, float* f);        /* current source buffer, SoA [19][ncell] */
+void orc_set_f(orc_lbm* o, const float* f);        /* into both buffers */
+long orc_bad_reads(const orc_lbm* o);               /* fluid pulls from geo-0 (unstored) cells */
+/* host residual of bifurcation.cu:1158-1175 on the current macros (long double sum, as double) */
+double orc_calc_res_bif(const orc_lbm* o);
+/* the reference's per-step residual sum (thrust::reduce emulated serially in fp32 over the
+ * reference storage order, ldc.cu:660-662) of the current macros */
+float orc_velsum(const orc_lbm* o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,38 @@
+"""Test configuration: `gpu` marks tests that need an MI355X (run with -m gpu on the GPU
+box); everything else runs on the CPU container.  The oracle (oracle/) is the checker."""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "lattice-boltzmann-method-gpu_amd")
+for p in (REPO, PKG, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
+    config.addinivalue_line("markers", "slow: long CPU-only oracle runs (excluded by default selection)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import orc
+    orc.build()
+    return orc
+
+
+@pytest.fixture(scope="session")
+def lbm():
+    import lbm_amd
+    return lbm_amd
+
+
+@pytest.fixture(scope="session")
+def gpu(lbm):
+    lbm.require_gpu()
+    return lbm
