@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py -- MLUPS of the D3Q19 BGK hot path on MI355X (one process per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (weak scaling): the lid-driven cavity of ldc.cu on a 512 x 512 x (512*N) box split
+into N z-slabs of 512^3 cells, one per GPU (N = 8 is BASELINE.json config C5, N = 1 the
+north-star 512^3 single-GPU lattice).  A step is one reference time step over the whole
+lattice: fused pull-stream + BGK collide with mask-driven bounce-back and lid NEE, the |u|
+residual reduction, and for N > 1 the RCCL halo exchange of the +-z faces (5 populations
+each) overlapped with the interior update plus the residual all-reduce.  Populations are
+resident in HBM before timing starts (generated on the device).
+
+Rank 0 prints ONE JSON line.  `value` = MLUPS over all ranks counting NX*NY*NZ box cells
+(SURVEY.md 8(d)); `roofline.achieved` = 152 B x fluid cells per step / average kernel time
+from HIP events recorded on the kernels' own stream; `cpu_baseline` = the serial oracle
+(oracle/, a port of the reference algorithm) on one host core, N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "lattice-boltzmann-method-gpu_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import torch  # noqa: E402  (before liblbm: one shared HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import lbm_amd  # noqa: E402
+from lbm_amd import cases  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_CELL = 152    # 19 fp32 loads + 19 fp32 stores per fluid cell update
+
+
+def cpu_baseline(n: int = 256, steps: int = 12):
+    """Serial oracle (reference algorithm restated in C, oracle/) on ONE host core, LDC n^3
+    (the C2 lattice), run as a child process with OMP_NUM_THREADS=1."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), str(n), str(steps)],
+                         env=env, capture_output=True, text=True, timeout=600, check=True)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    return {"value": round(r["mlups"], 3), "unit": "MLUPS", "cores": 1, "kind": "port",
+            "sample": f"oracle/lbm_oracle.c (serial C port of the reference kernels, fp32, two-phase LDC) "
+                      f"on LDC {n}^3 (config C2 lattice), {steps} steps after 1 warm-up, {r['seconds']:.1f} s, "
+                      f"1 thread (OMP_NUM_THREADS=1), host CPU: {r['cpu']}"}
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per launch measured by rocprofv3 PMC passes (tools/pmc_traffic.py writes it)."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        return d.get(workload, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def small_case_mlups(n: int, steps: int, dev: int):
+    lat = cases.ldc_device(n, n, n, device=dev)
+    lat.step(20, history=False)
+    lat.sync()
+    t = time.perf_counter()
+    lat.step(steps, history=False)
+    lat.sync()
+    dt = time.perf_counter() - t
+    lat.close()
+    return round(n ** 3 * steps / dt / 1e6, 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--n", type=int, default=512, help="per-GPU slab edge (nx = ny = nz_local)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    lbm_amd.require_gpu()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        cpu_group = dist.new_group(backend="gloo")
+
+    n = args.n
+    nzg = n * world
+    lat = cases.ldc_device(n, n, n, z_offset=rank * n, nz_global=nzg, device=local)
+    if world > 1:
+        obj = [lbm_amd.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=cpu_group)
+        lat.attach_rccl(obj[0], rank, world)
+    counts = lat.counts()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    lat.step(args.warmup, history=False)
+    lat.sync()
+    lat.profile(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lat.step(args.steps, history=False)
+    lat.sync()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    st = lat.stats()
+    state = lat.state()
+    elapsed = t1 - t0
+    kern_ms = st["kernel_ms"]
+    main_ms, main_n = st["stream_collide_ms"], max(1, st["stream_collide_launches"])
+    fix_ms = st["boundary_fixup_ms"]
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms, main_ms, fix_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms, main_ms, fix_ms = (float(v) for v in t)
+        fl = torch.tensor([counts["n_fluid"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(fl)
+        n_fluid_total = int(fl.item())
+    else:
+        n_fluid_total = counts["n_fluid"]
+    lat.close()
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    box_cells = n * n * nzg
+    ms_step = elapsed / args.steps * 1e3
+    mlups = box_cells * args.steps / elapsed / 1e6
+    # per-rank kernel time per step: stream-collide + boundary fix-up (edge + interior for N > 1)
+    kernel_step_ms = kern_ms / args.steps
+    achieved = BYTES_PER_CELL * counts["n_fluid"] / (kernel_step_ms * 1e-3) / 1e9
+    workload = f"ldc_{n}x{n}x{n}_per_gpu"
+    traffic = pmc_traffic(workload)
+    line = {
+        "metric": "MLUPS (million lattice updates/sec) + achieved HBM GB/s vs roofline",
+        "value": round(mlups, 1),
+        "unit": "MLUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (ldc.cu cavity generated on device: rho=1, u=0, lid u=0.15/C_U)",
+        "config": {
+            "workload": f"LDC D3Q19 BGK {n}x{n}x{nzg} box, z-slabs of {n}x{n}x{n} per GPU "
+                        f"(north-star 512^3 lattice at N=1; BASELINE config C5 at N=8)",
+            "global_shape_xyz": [n, n, nzg],
+            "box_cells": box_cells,
+            "fluid_cells": n_fluid_total,
+            "mlups_fluid_cells": round(n_fluid_total * args.steps / elapsed / 1e6, 1),
+            "parallelism": f"z-slab x{world}" + (" (RCCL halo, 5 pops/face)" if world > 1 else ""),
+            "tau": 0.55,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_stream_collide + k_boundary_fixup (one time step; 152 B x fluid cells)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algo_bytes_per_launch": BYTES_PER_CELL * counts["n_fluid"],
+            "avg_kernel_ms_per_step": round(kernel_step_ms, 4),
+            "avg_stream_collide_ms": round(main_ms / main_n, 4),
+            "avg_boundary_fixup_ms_per_step": round(fix_ms / args.steps, 4),
+            "boundary_cells_per_gpu": counts["n_boundary"],
+        },
+        "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
+        "residual_last": state["residual"],
+    }
+    if world == 1 and not args.no_secondary:
+        line["secondary"] = {"ldc64_mlups (published config)": small_case_mlups(64, 2000, local),
+                             "ldc256_mlups (config C2)": small_case_mlups(256, 200, local)}
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline()
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

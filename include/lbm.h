@@ -124,6 +124,11 @@ int lbm_get_counts(lbm_ctx* ctx, int64_t* n_box, int64_t* n_fluid, double* algo_
  * since enabling. */
 int lbm_profile(lbm_ctx* ctx, int enabled);
 int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
+/* The same split by kernel: kind 0 = fused stream-collide, 1 = boundary fix-up. */
+int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
+/* Fluid cells next to a non-equilibrium-extrapolation boundary (re-done by the boundary
+ * fix-up kernel each step). */
+int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
 
 /* Multi-GPU z-slabs (one process per GPU).  Rank 0 calls lbm_rccl_unique_id, the 128 bytes
  * are broadcast by the caller (e.g. torch.distributed), then every rank attaches.  After

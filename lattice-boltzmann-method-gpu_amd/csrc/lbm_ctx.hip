@@ -1,13 +1,16 @@
 // lbm_ctx.hip -- liblbm.so: the C ABI of include/lbm.h on top of the HIP kernels.
 //
 // A context owns one lattice (or one z-slab of it) on one device:
-//   two population buffers (A-B pattern; the reference's d_scr/d_dst, ldc.cu:640-641),
+//   two AoSoA population buffers (A-B pattern; the reference's d_scr/d_dst, ldc.cu:640-641),
 //   the cell-type bytes (the reference's d_geo + texture-bound index, Poiseulle.cu:49-50),
-//   (rho, u) arrays (d_rho/d_ux/d_uy/d_uz), block partials of the |u| sum and the
-//   device-resident state of the reference main loop (ldc.cu:613-685).
-// The reference's per-step launch sequence update -> boundary_stream -> calc_vel_square
-// -> thrust::reduce -> host residual (ldc.cu:654-684) becomes one fused collide-stream
-// launch plus a one-block finisher, with no host synchronisation inside a call.
+//   (rho, u) arrays (d_rho/d_ux/d_uy/d_uz), per-cell wall-link masks, per launch-range work
+//   lists (active 256-cell chunks, NEE-adjacent cells), block partials of the |u| sum and the device-resident
+//   state of the reference main loop (ldc.cu:613-685).
+// The reference's per-step sequence update -> boundary_stream -> calc_vel_square ->
+// thrust::reduce -> host residual (ldc.cu:654-684) becomes k_stream_collide +
+// k_boundary_fixup + a two-level deterministic reduction, with no host synchronisation
+// inside a call.  Slabs exchange the 5 populations crossing each +-z face (packed) over
+// RCCL on a second stream while the interior updates.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -28,6 +31,17 @@ namespace {
 std::string g_create_error;
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
+
+struct Range {            // one launch range of cells [c_lo, c_hi) with its work lists
+  int64_t c_lo = 0, c_hi = 0;
+  int* chunks = nullptr;  // active 256-cell chunks (>= 1 fluid cell in range)
+  int nchunks = 0;
+  int* cells = nullptr;   // NEE-adjacent fluid cells
+  int nslow = 0;
+  float4* prev = nullptr; // their (rho, u) of the previous step
+  double* part = nullptr; // main partials, then fix-up partials
+  int npart = 0;
+};
 }  // namespace
 
 struct lbm_ctx {
@@ -35,90 +49,72 @@ struct lbm_ctx {
   Layout L{};
   hipStream_t s_comp = nullptr, s_comm = nullptr;
   hipEvent_t ev_edge = nullptr, ev_halo = nullptr, ev_sum = nullptr, ev_fin = nullptr;
-  float* buf[2] = {nullptr, nullptr};
+  float* alloc[2] = {nullptr, nullptr};
+  float* buf[2] = {nullptr, nullptr};  // past the guard chunk
   uint8_t* type = nullptr;
+  uint32_t* links = nullptr;
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
-  double* partial = nullptr;
-  int grid_full = 0, grid_plane = 0;
+  Range whole, lo, hi, mid;  // single domain: whole; slabs: lo edge, hi edge, interior
+  double* partial_all = nullptr;
+  int npart_slab = 0;
+  double* scratch = nullptr;
   ConvState* conv = nullptr;
   float* hist = nullptr;
   int hist_cap = 0;
-  int steps_done = 0;      // device-confirmed steps
+  int* qsets = nullptr;  // device: up set (5), down set (5), all (19)
+  float *send_up = nullptr, *send_dn = nullptr, *recv_up = nullptr, *recv_dn = nullptr;
+  int steps_done = 0;    // device-confirmed steps
   bool bb_immediate = false;
   bool conv_enabled = false;
   bool halo_primed = false;
-  int64_t n_box = 0, n_fluid = 0;
+  int64_t n_box = 0, n_fluid = 0, n_slow = 0, n_wall_adj = 0;
   float tau = 0.f, omc = 0.f;
   // profiling
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
-  double kernel_ms = 0.0;
-  int64_t launches = 0;
+  std::vector<int> ev_kind;   // per recorded pair: 0 stream-collide, 1 boundary fix-up
+  double kernel_ms = 0.0, kind_ms[2] = {0.0, 0.0};
+  int64_t launches = 0, kind_n[2] = {0, 0};
   // rccl
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
   std::string err;
 };
 
-#define HIPCK(ctx, expr)                                                                    \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess) {                                                                 \
-      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                       \
-      return LBM_ERR_HIP;                                                                   \
-    }                                                                                       \
+#define HIPCK(ctx, expr)                                              \
+  do {                                                                \
+    hipError_t e_ = (expr);                                           \
+    if (e_ != hipSuccess) {                                           \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_); \
+      return LBM_ERR_HIP;                                             \
+    }                                                                 \
   } while (0)
 
-#define NCCK(ctx, expr)                                                                     \
-  do {                                                                                      \
-    ncclResult_t r_ = (expr);                                                               \
-    if (r_ != ncclSuccess) {                                                                \
-      (ctx)->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                      \
-      return LBM_ERR_RCCL;                                                                  \
-    }                                                                                       \
+#define NCCK(ctx, expr)                                                \
+  do {                                                                 \
+    ncclResult_t r_ = (expr);                                          \
+    if (r_ != ncclSuccess) {                                           \
+      (ctx)->err = std::string(#expr) + ": " + ncclGetErrorString(r_); \
+      return LBM_ERR_RCCL;                                             \
+    }                                                                  \
+  } while (0)
+
+#define RCK(expr)                  \
+  do {                             \
+    int rc_ = (expr);              \
+    if (rc_ != LBM_OK) return rc_; \
   } while (0)
 
 namespace {
 
-int fail(lbm_ctx* c, int code, const std::string& msg) {
-  c->err = msg;
-  return code;
+int64_t cell_of(const Layout& L, int x, int y, int z) {  // local z (storage plane z+1)
+  return (int64_t)x + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
 }
 
-float* pop(lbm_ctx* c, int b, int q) { return c->buf[b] + (int64_t)q * c->L.qstride; }
-float* src_buf(lbm_ctx* c) { return c->buf[c->steps_done & 1]; }
-
-StepArgs make_args(lbm_ctx* c, int hstep, int z_begin, int z_end, double* partial, bool store_all) {
-  StepArgs a{};
-  const bool first = (hstep == 0);
-  a.src = c->buf[hstep & 1];
-  a.dst = c->buf[(hstep + 1) & 1];
-  a.type = c->type;
-  a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
-  a.partial = partial;
-  a.qstride = c->L.qstride;
-  a.plane = c->L.plane;
-  a.pitch = c->L.pitch;
-  a.ny = c->L.ny;
-  a.z_begin = z_begin;
-  a.ntx = c->L.pitch / kTileX;
-  a.nty = (c->L.ny + kTileY - 1) / kTileY;
-  a.ntiles = a.ntx * a.nty * std::max(0, z_end - z_begin);
-  a.tau = c->tau;
-  a.omc = c->omc;
-  a.bb_active = (!first || c->bb_immediate) ? 1 : 0;
-  a.nee_active = first ? 0 : 1;
-  a.store_all_macros = store_all ? 1 : 0;
-  a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
-  return a;
-}
-
-int launch_cs(lbm_ctx* c, const StepArgs& a, int grid) {
-  if (a.ntiles <= 0) {
-    HIPCK(c, hipMemsetAsync(a.partial, 0, sizeof(double) * grid, c->s_comp));
-    return LBM_OK;
-  }
+// time one kernel launch with HIP events on its own stream (lbm_profile)
+template <class F>
+int timed(lbm_ctx* c, hipStream_t st, int kind, F&& launch) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof) {
     while (c->ev_pool.size() < c->ev_used + 2) {
@@ -128,24 +124,104 @@ int launch_cs(lbm_ctx* c, const StepArgs& a, int grid) {
     }
     e0 = c->ev_pool[c->ev_used++];
     e1 = c->ev_pool[c->ev_used++];
-    HIPCK(c, hipEventRecord(e0, c->s_comp));
+    c->ev_kind.push_back(kind);
+    HIPCK(c, hipEventRecord(e0, st));
   }
-  HIPCK(c, launch_collide_stream(a, grid, c->s_comp));
-  if (c->prof) HIPCK(c, hipEventRecord(e1, c->s_comp));
+  HIPCK(c, launch());
+  if (c->prof) HIPCK(c, hipEventRecord(e1, st));
   c->launches++;
+  c->kind_n[kind]++;
   return LBM_OK;
 }
 
 int harvest_profile(lbm_ctx* c) {
   if (c->ev_used == 0) return LBM_OK;
-  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  HIPCK(c, hipDeviceSynchronize());
   for (size_t i = 0; i + 1 < c->ev_used; i += 2) {
     float ms = 0.f;
     HIPCK(c, hipEventElapsedTime(&ms, c->ev_pool[i], c->ev_pool[i + 1]));
     c->kernel_ms += ms;
+    c->kind_ms[c->ev_kind[i / 2]] += ms;
   }
   c->ev_used = 0;
+  c->ev_kind.clear();
   return LBM_OK;
+}
+
+// one step's update of a range: main kernel over the active chunks, then the boundary
+// fix-up of the listed cells (same stream: the fix-up overwrites what the main kernel stored)
+int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
+  const bool first = (hstep == 0);
+  const float* src = c->buf[hstep & 1];
+  float* dst = c->buf[(hstep + 1) & 1];
+  const int* stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
+  if (r.nchunks > 0) {
+    MainArgs a{};
+    a.src = src; a.dst = dst; a.type = c->type; a.links = c->links;
+    a.bb_active = (!first || c->bb_immediate) ? 1 : 0;
+    a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
+    a.partial = r.part;
+    a.chunks = r.chunks; a.nchunks = r.nchunks;
+    a.pitch = c->L.pitch; a.plane = c->L.plane;
+    a.c_lo = r.c_lo; a.c_hi = r.c_hi;
+    a.tau = c->tau;
+    a.store_all_macros = store_all ? 1 : 0;
+    a.stopped = stopped;
+    RCK(timed(c, st, 0, [&] { return launch_main(a, st); }));
+  }
+  if (r.nslow > 0) {
+    FixArgs f{};
+    f.src = src; f.dst = dst; f.type = c->type;
+    f.rho = c->rho; f.ux = c->ux; f.uy = c->uy; f.uz = c->uz;
+    f.prev = r.prev; f.cells = r.cells; f.n = r.nslow;
+    f.pitch = c->L.pitch; f.plane = c->L.plane;
+    f.tau = c->tau; f.omc = c->omc;
+    f.bb_active = (!first || c->bb_immediate) ? 1 : 0;
+    f.nee_active = first ? 0 : 1;
+    f.store_all_macros = store_all ? 1 : 0;
+    f.partial = r.part + (r.nchunks > 0 ? main_grid(r.nchunks) : 0);
+    f.stopped = stopped;
+    RCK(timed(c, st, 1, [&] { return launch_fix(f, st); }));
+  }
+  return LBM_OK;
+}
+
+// work lists of the cell range [lo, hi) from the host copy of the type bytes
+int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t) {
+  r.c_lo = lo;
+  r.c_hi = hi;
+  std::vector<int> chunks, cells;
+  for (int64_t ch = lo / kChunk; ch * kChunk < hi; ++ch) {
+    bool any = false;
+    for (int64_t k = std::max(lo, ch * kChunk); k < std::min(hi, (ch + 1) * kChunk); ++k) {
+      const uint8_t v = t[k];
+      if ((v & kClassMask) != kFluid) continue;
+      any = true;
+      if (v & kNeedsMac) cells.push_back((int)k);
+    }
+    if (any) chunks.push_back((int)ch);
+  }
+  r.nchunks = (int)chunks.size();
+  r.nslow = (int)cells.size();
+  if (r.nchunks) {
+    HIPCK(c, hipMalloc(&r.chunks, sizeof(int) * r.nchunks));
+    HIPCK(c, hipMemcpy(r.chunks, chunks.data(), sizeof(int) * r.nchunks, hipMemcpyHostToDevice));
+  }
+  if (r.nslow) {
+    HIPCK(c, hipMalloc(&r.cells, sizeof(int) * r.nslow));
+    HIPCK(c, hipMemcpy(r.cells, cells.data(), sizeof(int) * r.nslow, hipMemcpyHostToDevice));
+    HIPCK(c, hipMalloc(&r.prev, sizeof(float4) * r.nslow));
+    HIPCK(c, hipMemset(r.prev, 0, sizeof(float4) * r.nslow));
+  }
+  r.npart = (r.nchunks ? main_grid(r.nchunks) : 0) + (r.nslow ? fix_grid(r.nslow) : 0);
+  return LBM_OK;
+}
+
+void free_range(Range& r) {
+  if (r.chunks) (void)hipFree(r.chunks);
+  if (r.cells) (void)hipFree(r.cells);
+  if (r.prev) (void)hipFree(r.prev);
+  r = Range{};
 }
 
 int ensure_hist(lbm_ctx* c, int n) {
@@ -158,39 +234,36 @@ int ensure_hist(lbm_ctx* c, int n) {
 
 // fresh main-loop state (k = 0, sum_current = 0) keeping the convergence settings
 int reset_state(lbm_ctx* c) {
-  ConvState cs{};
-  ConvState host{};
+  ConvState cs{}, host{};
   HIPCK(c, hipMemcpy(&host, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
   cs.enabled = host.enabled;
   cs.max_it = host.max_it;
   cs.stag_max = host.stag_max;
   cs.tol = host.tol;
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
+  for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid})
+    if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
   c->steps_done = 0;
   c->halo_primed = false;
   return LBM_OK;
-}
-
-// raster [nz][ny][nx] (local planes) <-> storage offsets
-int64_t sidx(const Layout& L, int x, int y, int z) {
-  return (int64_t)x + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
 }
 
 }  // namespace
 
 extern "C" {
 
-const char* lbm_version(void) { return "lbm-mi355x 0.1 (gfx950, D3Q19 BGK fused pull/collide)"; }
+const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA wave-chunk stream-collide)"; }
 
-const char* lbm_last_error(const lbm_ctx* ctx) {
-  return ctx ? ctx->err.c_str() : g_create_error.c_str();
-}
+const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
-  if (!desc || !out) { g_create_error = "null argument"; return LBM_ERR_ARG; }
+  if (!desc || !out) {
+    g_create_error = "null argument";
+    return LBM_ERR_ARG;
+  }
   *out = nullptr;
   const lbm_desc& d = *desc;
-  if (d.nx < 3 || d.ny < 3 || d.nz < 1 || d.tau <= 0.f || d.case_kind < 0 || d.case_kind > 2) {
+  if (d.nx < 3 || d.ny < 3 || d.nz < 1 || !(d.tau > 0.f) || d.case_kind < 0 || d.case_kind > 2) {
     g_create_error = "invalid lattice description";
     return LBM_ERR_ARG;
   }
@@ -200,87 +273,88 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   }
   lbm_ctx* c = new lbm_ctx();
   c->d = d;
-  c->d.geo = nullptr; c->d.bc_inlet_uy = nullptr; c->d.bc_outlet_uy = nullptr;
+  c->d.geo = nullptr;
+  c->d.bc_inlet_uy = nullptr;
+  c->d.bc_outlet_uy = nullptr;
   if (c->d.nz_global <= 0) c->d.nz_global = d.nz;
   c->tau = d.tau;
   c->omc = 1.0f - 1.0f / d.tau;  // the reference's (1.0f - 1.0f / tau), evaluated in fp32
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
-  L.pitch = (d.nx + kTileX - 1) / kTileX * kTileX;
+  L.pitch = (d.nx + 3) / 4 * 4;
   L.planes = d.nz + 2;
   L.plane = (int64_t)L.pitch * L.ny;
-  const int64_t ncs = L.plane * L.planes;
-  L.qstride = (ncs + 63) / 64 * 64;
-  if (ncs >= (int64_t(1) << 30)) {
-    g_create_error = "slab too large for 32-bit cell offsets (use more z-slabs)";
+  L.ncell = (L.plane * L.planes + kChunk - 1) / kChunk * kChunk;
+  L.nchunk = L.ncell / kChunk;
+  L.guard = (L.plane + L.pitch + 8 + kChunk - 1) / kChunk + 1;
+  c->n_box = (int64_t)d.nx * d.ny * d.nz;
+  if (L.ncell >= (int64_t(1) << 31) - 2 * kChunk) {
+    g_create_error = "slab too large for 32-bit cell ids (split it into more z-slabs)";
     delete c;
     return LBM_ERR_ARG;
   }
-  c->n_box = (int64_t)d.nx * d.ny * d.nz;
 
   auto bail = [&](int code) {
     g_create_error = c->err;
     lbm_destroy(c);
     return code;
   };
-#define CK(expr)                                                   \
-  do {                                                             \
-    hipError_t e_ = (expr);                                        \
-    if (e_ != hipSuccess) {                                        \
-      c->err = std::string(#expr) + ": " + hipGetErrorString(e_);  \
-      return bail(LBM_ERR_HIP);                                    \
-    }                                                              \
+#define CK(expr)                                                  \
+  do {                                                            \
+    hipError_t e_ = (expr);                                       \
+    if (e_ != hipSuccess) {                                       \
+      c->err = std::string(#expr) + ": " + hipGetErrorString(e_); \
+      return bail(LBM_ERR_HIP);                                   \
+    }                                                             \
   } while (0)
 
   CK(hipSetDevice(d.device));
   CK(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking));
-  CK(hipEventCreateWithFlags(&c->ev_edge, hipEventDisableTiming));
-  CK(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
-  CK(hipEventCreateWithFlags(&c->ev_sum, hipEventDisableTiming));
-  CK(hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming));
-  CK(hipMalloc(&c->buf[0], sizeof(float) * 19 * L.qstride));
-  CK(hipMalloc(&c->buf[1], sizeof(float) * 19 * L.qstride));
-  CK(hipMalloc(&c->type, L.qstride));
-  CK(hipMalloc(&c->rho, sizeof(float) * L.qstride));
-  CK(hipMalloc(&c->ux, sizeof(float) * L.qstride));
-  CK(hipMalloc(&c->uy, sizeof(float) * L.qstride));
-  CK(hipMalloc(&c->uz, sizeof(float) * L.qstride));
+  for (hipEvent_t* e : {&c->ev_edge, &c->ev_halo, &c->ev_sum, &c->ev_fin})
+    CK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (int b = 0; b < 2; ++b) {
+    CK(hipMalloc(&c->alloc[b], sizeof(float) * L.buf_floats()));
+    c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
+    CK(hipMemsetAsync(c->alloc[b], 0, sizeof(float) * L.buf_floats(), c->s_comp));
+  }
+  CK(hipMalloc(&c->type, L.ncell));
+  CK(hipMalloc(&c->links, sizeof(uint32_t) * L.ncell));
+  CK(hipMemsetAsync(c->links, 0, sizeof(uint32_t) * L.ncell, c->s_comp));
+  for (float** p : {&c->rho, &c->ux, &c->uy, &c->uz}) {
+    CK(hipMalloc(p, sizeof(float) * L.ncell));
+    CK(hipMemsetAsync(*p, 0, sizeof(float) * L.ncell, c->s_comp));
+  }
   CK(hipMalloc(&c->conv, sizeof(ConvState)));
   CK(hipMemsetAsync(c->conv, 0, sizeof(ConvState), c->s_comp));
-  for (float* p : {c->rho, c->ux, c->uy, c->uz}) CK(hipMemsetAsync(p, 0, sizeof(float) * L.qstride, c->s_comp));
-  CK(hipMemsetAsync(c->type, 0, L.qstride, c->s_comp));
+  CK(hipMalloc(&c->scratch, sizeof(double) * kReduceBlocks));
+  {
+    int h[29];
+    for (int k = 0; k < 5; ++k) {
+      h[k] = kUpSet[k];
+      h[5 + k] = kDownSet[k];
+    }
+    for (int q = 0; q < kQ; ++q) h[10 + q] = q;
+    CK(hipMalloc(&c->qsets, sizeof(h)));
+    CK(hipMemcpy(c->qsets, h, sizeof(h), hipMemcpyHostToDevice));
+  }
 
-  // grid: enough resident blocks to fill the chip, each striding over 64x4 tiles
-  int ncu = 256;
-  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d.device));
-  const int occ = 8;  // resident 256-thread blocks per CU the grid is sized for
-  const int ntx = L.pitch / kTileX, nty = (L.ny + kTileY - 1) / kTileY;
-  const int64_t tiles_full = (int64_t)ntx * nty * d.nz, tiles_plane = (int64_t)ntx * nty;
-  c->grid_full = (int)std::max<int64_t>(1, std::min<int64_t>(tiles_full, (int64_t)ncu * occ));
-  c->grid_plane = (int)std::max<int64_t>(1, std::min<int64_t>(tiles_plane, (int64_t)ncu * occ));
-  // partial slots: [full | edge lo | edge hi | interior]
-  CK(hipMalloc(&c->partial, sizeof(double) * (c->grid_full + 2 * c->grid_plane + c->grid_full)));
-
-  // ---- geometry: reference codes in storage layout -> type bytes ----
+  // ---- geometry: reference codes per linear cell -> type bytes ----
   int8_t* dcodes = nullptr;
-  CK(hipMalloc(&dcodes, L.qstride));
-  CK(hipMemsetAsync(dcodes, 0, L.qstride, c->s_comp));
+  CK(hipMalloc(&dcodes, L.ncell));
+  CK(hipMemsetAsync(dcodes, 0, L.ncell, c->s_comp));
   float *din = nullptr, *dout = nullptr;
-  if (d.geo) {
-    std::vector<int8_t> h((size_t)ncs, 0);
+  if (desc->geo) {
+    std::vector<int8_t> h((size_t)L.ncell, 0);
     const int zlo = d.halo_planes ? -1 : 0, zhi = d.halo_planes ? d.nz + 1 : d.nz;
     for (int z = zlo; z < zhi; ++z)
-      for (int y = 0; y < d.ny; ++y) {
-        const int8_t* srow = d.geo + ((int64_t)(z - zlo) * d.ny + y) * d.nx;
-        std::memcpy(&h[sidx(L, 0, y, z)], srow, d.nx);
-      }
-    CK(hipMemcpyAsync(dcodes, h.data(), ncs, hipMemcpyHostToDevice, c->s_comp));
+      for (int y = 0; y < d.ny; ++y)
+        std::memcpy(&h[cell_of(L, 0, y, z)], desc->geo + ((int64_t)(z - zlo) * d.ny + y) * d.nx, d.nx);
+    CK(hipMemcpyAsync(dcodes, h.data(), L.ncell, hipMemcpyHostToDevice, c->s_comp));
     CK(hipStreamSynchronize(c->s_comp));
   } else {
-    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.planes, L.plane, d.z_offset, c->d.nz_global,
-                        c->s_comp));
+    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.plane, L.ncell, d.z_offset, c->d.nz_global, c->s_comp));
   }
   const int64_t ntab = (int64_t)d.nx * c->d.nz_global;
   if (desc->bc_inlet_uy) {
@@ -292,13 +366,12 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     CK(hipMemcpy(dout, desc->bc_outlet_uy, sizeof(float) * ntab, hipMemcpyHostToDevice));
   }
   GeoArgs g{};
-  g.codes = dcodes; g.type = c->type;
+  g.codes = dcodes; g.type = c->type; g.links = c->links;
   g.rho = c->rho; g.ux = c->ux; g.uy = c->uy; g.uz = c->uz;
   g.inlet_uy = din; g.outlet_uy = dout;
   g.case_kind = d.case_kind; g.lid_u = d.lid_u;
-  g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.planes = L.planes; g.plane = L.plane;
-  g.z_offset = d.z_offset;
-  g.nz_global = c->d.nz_global;
+  g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.plane = L.plane; g.ncell = L.ncell;
+  g.z_offset = d.z_offset; g.nz_global = c->d.nz_global;
   CK(launch_classify(g, c->s_comp));
   CK(launch_flag_fluid(g, c->s_comp));
   CK(hipStreamSynchronize(c->s_comp));
@@ -306,16 +379,38 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   if (din) CK(hipFree(din));
   if (dout) CK(hipFree(dout));
 
-  // count fluid cells of the local planes
+  // ---- work lists: whole domain, and lo edge / hi edge / interior for slabs ----
   {
-    std::vector<uint8_t> t((size_t)ncs);
-    CK(hipMemcpy(t.data(), c->type, ncs, hipMemcpyDeviceToHost));
+    std::vector<uint8_t> t((size_t)L.ncell);
+    CK(hipMemcpy(t.data(), c->type, L.ncell, hipMemcpyDeviceToHost));
     int64_t nf = 0;
     for (int z = 0; z < d.nz; ++z)
       for (int y = 0; y < d.ny; ++y)
-        for (int x = 0; x < d.nx; ++x)
-          if ((t[sidx(L, x, y, z)] & kClassMask) == kFluid) ++nf;
+        for (int x = 0; x < d.nx; ++x) {
+          const uint8_t v = t[cell_of(L, x, y, z)];
+          if ((v & kClassMask) != kFluid) continue;
+          ++nf;
+          if (v & kNeedsMac) ++c->n_slow;
+          if (v & kWallAdj) ++c->n_wall_adj;
+          // a fluid cell on the outer x/y layer would pull across rows
+          if (x == 0 || x == d.nx - 1 || y == 0 || y == d.ny - 1) {
+            c->err = "fluid cell on the outer x/y layer of the box";
+            return bail(LBM_ERR_GEOMETRY);
+          }
+        }
     c->n_fluid = nf;
+    const int64_t P = L.plane, nz = d.nz;
+    if (build_range(c, c->whole, P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->lo, P, 2 * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (nz > 1 && build_range(c, c->hi, nz * P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t) != LBM_OK) return bail(LBM_ERR_HIP);
+    // partial slots: [whole | lo | hi | mid]; the slab ranges are contiguous
+    c->npart_slab = c->lo.npart + c->hi.npart + c->mid.npart;
+    CK(hipMalloc(&c->partial_all, sizeof(double) * std::max(1, c->whole.npart + c->npart_slab)));
+    c->whole.part = c->partial_all;
+    c->lo.part = c->whole.part + c->whole.npart;
+    c->hi.part = c->lo.part + c->lo.npart;
+    c->mid.part = c->hi.part + c->hi.npart;
   }
 #undef CK
   *out = c;
@@ -328,11 +423,16 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->s_comp) (void)hipStreamSynchronize(c->s_comp);
   if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  for (float* p : {c->buf[0], c->buf[1], c->rho, c->ux, c->uy, c->uz, c->hist})
+  for (float* p : {c->alloc[0], c->alloc[1], c->rho, c->ux, c->uy, c->uz, c->hist, c->send_up, c->send_dn,
+                   c->recv_up, c->recv_dn})
     if (p) (void)hipFree(p);
+  for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid}) free_range(*r);
   if (c->type) (void)hipFree(c->type);
-  if (c->partial) (void)hipFree(c->partial);
+  if (c->links) (void)hipFree(c->links);
+  if (c->partial_all) (void)hipFree(c->partial_all);
+  if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
+  if (c->qsets) (void)hipFree(c->qsets);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->ev_edge, c->ev_halo, c->ev_sum, c->ev_fin})
     if (e) (void)hipEventDestroy(e);
@@ -341,26 +441,24 @@ void lbm_destroy(lbm_ctx* c) {
   delete c;
 }
 
-int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux, const float* uy,
-                         const float* uz) {
+int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux, const float* uy, const float* uz) {
   if (!c || (form != LBM_INIT_LDC_WI && form != LBM_INIT_EXPANDED)) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
   const Layout& L = c->L;
-  const int64_t ncs = L.plane * L.planes;
   const float* host[4] = {rho, ux, uy, uz};
   float* dev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<float> h;
   for (int k = 0; k < 4; ++k) {
     if (!host[k]) continue;
-    h.assign((size_t)ncs, k == 0 ? 1.0f : 0.0f);
+    h.assign((size_t)L.ncell, k == 0 ? 1.0f : 0.0f);
     for (int z = 0; z < L.nz; ++z)
       for (int y = 0; y < L.ny; ++y)
-        std::memcpy(&h[sidx(L, 0, y, z)], host[k] + ((int64_t)z * L.ny + y) * L.nx, sizeof(float) * L.nx);
-    HIPCK(c, hipMalloc(&dev[k], sizeof(float) * ncs));
-    HIPCK(c, hipMemcpy(dev[k], h.data(), sizeof(float) * ncs, hipMemcpyHostToDevice));
+        std::memcpy(&h[cell_of(L, 0, y, z)], host[k] + ((int64_t)z * L.ny + y) * L.nx, sizeof(float) * L.nx);
+    HIPCK(c, hipMalloc(&dev[k], sizeof(float) * L.ncell));
+    HIPCK(c, hipMemcpy(dev[k], h.data(), sizeof(float) * L.ncell, hipMemcpyHostToDevice));
   }
-  HIPCK(c, launch_init_feq(c->buf[0], c->buf[1], L.qstride, ncs, form == LBM_INIT_LDC_WI ? 0 : 1, dev[0],
-                           dev[1], dev[2], dev[3], c->s_comp));
+  HIPCK(c, launch_init_feq(c->buf[0], c->buf[1], L.ncell, form == LBM_INIT_LDC_WI ? 0 : 1, dev[0], dev[1], dev[2],
+                           dev[3], c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   for (float* p : dev)
     if (p) HIPCK(c, hipFree(p));
@@ -370,9 +468,7 @@ int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux
 int lbm_init_ldc(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
-  const Layout& L = c->L;
-  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], L.qstride, L.nx, L.ny, L.pitch, L.planes, L.plane,
-                           c->d.z_offset, c->d.lid_u, c->s_comp));
+  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.ny, c->d.lid_u, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -381,15 +477,15 @@ int lbm_set_f(lbm_ctx* c, const float* f) {
   if (!c || !f) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
   const Layout& L = c->L;
-  std::vector<float> h((size_t)L.qstride, 0.f);
-  for (int q = 0; q < 19; ++q) {
+  std::vector<float> h((size_t)L.nchunk * kQ * kChunk, 0.f);
+  for (int q = 0; q < kQ; ++q)
     for (int z = 0; z < L.nz; ++z)
-      for (int y = 0; y < L.ny; ++y)
-        std::memcpy(&h[sidx(L, 0, y, z)], f + (((int64_t)q * L.nz + z) * L.ny + y) * L.nx,
-                    sizeof(float) * L.nx);
-    HIPCK(c, hipMemcpy(pop(c, 0, q), h.data(), sizeof(float) * L.qstride, hipMemcpyHostToDevice));
-    HIPCK(c, hipMemcpy(pop(c, 1, q), h.data(), sizeof(float) * L.qstride, hipMemcpyHostToDevice));
-  }
+      for (int y = 0; y < L.ny; ++y) {
+        const float* row = f + (((int64_t)q * L.nz + z) * L.ny + y) * L.nx;
+        for (int x = 0; x < L.nx; ++x) h[aidx(cell_of(L, x, y, z), q)] = row[x];
+      }
+  for (int b = 0; b < 2; ++b)
+    HIPCK(c, hipMemcpy(c->buf[b], h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
   return reset_state(c);
 }
 
@@ -415,56 +511,70 @@ namespace {
 
 // ---- halo exchange (slabs) ----------------------------------------------------------------
 
-// RCCL: send the top local plane's up-going populations to rank+1 (into its bottom ghost plane)
-// and the bottom plane's down-going populations to rank-1 (into its top ghost plane).
-int rccl_exchange(lbm_ctx* c, int b, int npops_all) {
-  const Layout& L = c->L;
-  const size_t cnt = (size_t)L.plane;
-  NCCK(c, ncclGroupStart());
+int ensure_halo_buffers(lbm_ctx* c) {
+  if (c->send_up) return LBM_OK;
+  const size_t bytes = sizeof(float) * kQ * (size_t)c->L.plane;
+  for (float** p : {&c->send_up, &c->send_dn, &c->recv_up, &c->recv_dn}) HIPCK(c, hipMalloc(p, bytes));
+  return LBM_OK;
+}
+
+const int* qset(lbm_ctx* c, int which) { return c->qsets + (which == 0 ? 0 : which == 1 ? 5 : 10); }
+
+// pack this slab's outgoing faces of buffer b: the top plane's up-going populations and the
+// bottom plane's down-going ones (all 19 when `all`)
+int pack_faces(lbm_ctx* c, int b, bool all, hipStream_t st) {
+  const int nq = all ? kQ : 5;
+  HIPCK(c, launch_pack(c->buf[b], c->send_up, c->L.nz, c->L.plane, all ? qset(c, 2) : qset(c, 0), nq, st));
+  HIPCK(c, launch_pack(c->buf[b], c->send_dn, 1, c->L.plane, all ? qset(c, 2) : qset(c, 1), nq, st));
+  return LBM_OK;
+}
+
+// unpack what arrived into the ghost planes of buffer b
+int unpack_faces(lbm_ctx* c, int b, bool all, bool from_dn, bool from_up, hipStream_t st) {
+  const int nq = all ? kQ : 5;
+  if (from_dn) HIPCK(c, launch_unpack(c->buf[b], c->recv_dn, 0, c->L.plane, all ? qset(c, 2) : qset(c, 0), nq, st));
+  if (from_up)
+    HIPCK(c, launch_unpack(c->buf[b], c->recv_up, c->L.nz + 1, c->L.plane, all ? qset(c, 2) : qset(c, 1), nq, st));
+  return LBM_OK;
+}
+
+int rccl_exchange(lbm_ctx* c, int b, bool all) {
+  const size_t cnt = (size_t)(all ? kQ : 5) * c->L.plane;
   const int up = c->rank + 1 < c->nranks ? c->rank + 1 : -1;
   const int dn = c->rank > 0 ? c->rank - 1 : -1;
-  for (int k = 0; k < (npops_all ? 19 : 5); ++k) {
-    const int qu = npops_all ? k : kUpSet[k];
-    const int qd = npops_all ? k : kDownSet[k];
-    if (up >= 0) {
-      NCCK(c, ncclSend(pop(c, b, qu) + (int64_t)L.nz * L.plane, cnt, ncclFloat, up, c->comm, c->s_comm));
-      NCCK(c, ncclRecv(pop(c, b, qd) + (int64_t)(L.nz + 1) * L.plane, cnt, ncclFloat, up, c->comm, c->s_comm));
-    }
-    if (dn >= 0) {
-      NCCK(c, ncclSend(pop(c, b, qd) + (int64_t)1 * L.plane, cnt, ncclFloat, dn, c->comm, c->s_comm));
-      NCCK(c, ncclRecv(pop(c, b, qu) + 0, cnt, ncclFloat, dn, c->comm, c->s_comm));
-    }
+  RCK(pack_faces(c, b, all, c->s_comp));
+  HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
+  HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
+  NCCK(c, ncclGroupStart());
+  if (up >= 0) {
+    NCCK(c, ncclSend(c->send_up, cnt, ncclFloat, up, c->comm, c->s_comm));
+    NCCK(c, ncclRecv(c->recv_up, cnt, ncclFloat, up, c->comm, c->s_comm));
+  }
+  if (dn >= 0) {
+    NCCK(c, ncclSend(c->send_dn, cnt, ncclFloat, dn, c->comm, c->s_comm));
+    NCCK(c, ncclRecv(c->recv_dn, cnt, ncclFloat, dn, c->comm, c->s_comm));
   }
   NCCK(c, ncclGroupEnd());
+  RCK(unpack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
+  HIPCK(c, hipEventRecord(c->ev_halo, c->s_comm));
   return LBM_OK;
 }
 
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
-  const Layout& L = c->L;
   int h = c->steps_done;
   for (int s = 0; s < nsteps; ++s, ++h) {
     const bool store_all = c->conv_enabled || (s == nsteps - 1);
-    StepArgs a = make_args(c, h, 1, L.nz + 1, c->partial, store_all);
-    int rc = launch_cs(c, a, c->grid_full);
-    if (rc) return rc;
-    HIPCK(c, launch_finish(c->partial, c->grid_full, c->conv, want_hist ? c->hist + s : nullptr, 1,
-                           c->s_comp));
+    RCK(run_range(c, c->whole, h, store_all, c->s_comp));
+    HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
+                           1, c->s_comp));
   }
   return LBM_OK;
 }
 
 int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
-  const Layout& L = c->L;
-  double* p_lo = c->partial + c->grid_full;
-  double* p_hi = p_lo + c->grid_plane;
-  double* p_in = p_hi + c->grid_plane;
-  const int n_part = 2 * c->grid_plane + c->grid_full;
-  if (!c->halo_primed) {  // initial ghost planes of the source buffer: all 19 populations
-    HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
-    HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
-    int rc = rccl_exchange(c, c->steps_done & 1, 1);
-    if (rc) return rc;
-    HIPCK(c, hipEventRecord(c->ev_halo, c->s_comm));
+  RCK(ensure_halo_buffers(c));
+  if (!c->halo_primed) {  // ghost planes of the initial source buffer: all 19 populations
+    RCK(rccl_exchange(c, c->steps_done & 1, true));
     c->halo_primed = true;
   }
   int h = c->steps_done;
@@ -472,27 +582,12 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     const bool store_all = c->conv_enabled || (s == nsteps - 1);
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
-    // edge planes first, so their halo can travel while the interior runs
-    StepArgs lo = make_args(c, h, 1, 2, p_lo, store_all);
-    int rc = launch_cs(c, lo, c->grid_plane);
-    if (rc) return rc;
-    if (L.nz > 1) {
-      StepArgs hi = make_args(c, h, L.nz, L.nz + 1, p_hi, store_all);
-      rc = launch_cs(c, hi, c->grid_plane);
-      if (rc) return rc;
-    } else {
-      HIPCK(c, hipMemsetAsync(p_hi, 0, sizeof(double) * c->grid_plane, c->s_comp));
-    }
-    HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
-    HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
-    rc = rccl_exchange(c, (h + 1) & 1, 0);
-    if (rc) return rc;
-    HIPCK(c, hipEventRecord(c->ev_halo, c->s_comm));
-    // interior planes overlap the exchange
-    StepArgs in = make_args(c, h, 2, L.nz, p_in, store_all);
-    rc = launch_cs(c, in, c->grid_full);
-    if (rc) return rc;
-    HIPCK(c, launch_finish(p_lo, n_part, c->conv, nullptr, 0, c->s_comp));
+    // edge planes first, so their halo travels while the interior runs
+    RCK(run_range(c, c->lo, h, store_all, c->s_comp));
+    if (c->L.nz > 1) RCK(run_range(c, c->hi, h, store_all, c->s_comp));
+    RCK(rccl_exchange(c, (h + 1) & 1, false));
+    RCK(run_range(c, c->mid, h, store_all, c->s_comp));
+    HIPCK(c, launch_reduce(c->lo.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp));
     HIPCK(c, hipEventRecord(c->ev_sum, c->s_comp));
     HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_sum, 0));
     NCCK(c, ncclAllReduce(&c->conv->s_local, &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
@@ -517,12 +612,10 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
   HIPCK(c, hipSetDevice(c->d.device));
   const bool want_hist = residual_hist != nullptr;
   if (want_hist) {
-    int rc = ensure_hist(c, nsteps);
-    if (rc) return rc;
-    HIPCK(c, hipMemsetAsync(c->hist, 0xFF, sizeof(float) * nsteps, c->s_comp));  // NaN: not run
+    RCK(ensure_hist(c, nsteps));
+    HIPCK(c, hipMemsetAsync(c->hist, 0xFF, sizeof(float) * nsteps, c->s_comp));  // NaN: step not run
   }
-  int rc = c->comm ? step_rccl(c, nsteps, want_hist) : step_single(c, nsteps, want_hist);
-  if (rc) return rc;
+  RCK(c->comm ? step_rccl(c, nsteps, want_hist) : step_single(c, nsteps, want_hist));
   const bool sync = want_hist || steps_done || c->conv_enabled;
   if (sync) {
     HIPCK(c, hipStreamSynchronize(c->s_comp));
@@ -548,9 +641,7 @@ int lbm_sync(lbm_ctx* c) {
 
 int lbm_get_state(lbm_ctx* c, int* k, int* tol_count, int* stopped, float* residual, double* velsum) {
   if (!c) return LBM_ERR_ARG;
-  HIPCK(c, hipSetDevice(c->d.device));
-  int rc = lbm_sync(c);
-  if (rc) return rc;
+  RCK(lbm_sync(c));
   ConvState h{};
   HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
   if (k) *k = h.k;
@@ -563,22 +654,20 @@ int lbm_get_state(lbm_ctx* c, int* k, int* tol_count, int* stopped, float* resid
 
 int lbm_get_macros(lbm_ctx* c, float* rho, float* ux, float* uy, float* uz) {
   if (!c) return LBM_ERR_ARG;
-  int rc = lbm_sync(c);
-  if (rc) return rc;
+  RCK(lbm_sync(c));
   const Layout& L = c->L;
-  const int64_t ncs = L.plane * L.planes;
-  std::vector<uint8_t> t((size_t)ncs);
-  HIPCK(c, hipMemcpy(t.data(), c->type, ncs, hipMemcpyDeviceToHost));
-  std::vector<float> h((size_t)ncs);
+  std::vector<uint8_t> t((size_t)L.ncell);
+  HIPCK(c, hipMemcpy(t.data(), c->type, L.ncell, hipMemcpyDeviceToHost));
+  std::vector<float> h((size_t)L.ncell);
   float* outs[4] = {rho, ux, uy, uz};
   float* devs[4] = {c->rho, c->ux, c->uy, c->uz};
   for (int k = 0; k < 4; ++k) {
     if (!outs[k]) continue;
-    HIPCK(c, hipMemcpy(h.data(), devs[k], sizeof(float) * ncs, hipMemcpyDeviceToHost));
+    HIPCK(c, hipMemcpy(h.data(), devs[k], sizeof(float) * L.ncell, hipMemcpyDeviceToHost));
     for (int z = 0; z < L.nz; ++z)
       for (int y = 0; y < L.ny; ++y)
         for (int x = 0; x < L.nx; ++x) {
-          const int64_t s = sidx(L, x, y, z);
+          const int64_t s = cell_of(L, x, y, z);
           outs[k][((int64_t)z * L.ny + y) * L.nx + x] = ((t[s] & kClassMask) == kFluid) ? h[s] : 0.0f;
         }
   }
@@ -587,16 +676,16 @@ int lbm_get_macros(lbm_ctx* c, float* rho, float* ux, float* uy, float* uz) {
 
 int lbm_get_f(lbm_ctx* c, float* f) {
   if (!c || !f) return LBM_ERR_ARG;
-  int rc = lbm_sync(c);
-  if (rc) return rc;
+  RCK(lbm_sync(c));
   const Layout& L = c->L;
-  std::vector<float> h((size_t)L.qstride);
-  for (int q = 0; q < 19; ++q) {
-    HIPCK(c, hipMemcpy(h.data(), pop(c, c->steps_done & 1, q), sizeof(float) * L.qstride, hipMemcpyDeviceToHost));
+  std::vector<float> h((size_t)L.nchunk * kQ * kChunk);
+  HIPCK(c, hipMemcpy(h.data(), c->buf[c->steps_done & 1], sizeof(float) * h.size(), hipMemcpyDeviceToHost));
+  for (int q = 0; q < kQ; ++q)
     for (int z = 0; z < L.nz; ++z)
-      for (int y = 0; y < L.ny; ++y)
-        std::memcpy(f + (((int64_t)q * L.nz + z) * L.ny + y) * L.nx, &h[sidx(L, 0, y, z)], sizeof(float) * L.nx);
-  }
+      for (int y = 0; y < L.ny; ++y) {
+        float* row = f + (((int64_t)q * L.nz + z) * L.ny + y) * L.nx;
+        for (int x = 0; x < L.nx; ++x) row[x] = h[aidx(cell_of(L, x, y, z), q)];
+      }
   return LBM_OK;
 }
 
@@ -608,20 +697,34 @@ int lbm_get_counts(lbm_ctx* c, int64_t* n_box, int64_t* n_fluid, double* algo_by
   return LBM_OK;
 }
 
+int lbm_get_boundary_cells(lbm_ctx* c, int64_t* n_boundary) {
+  if (!c || !n_boundary) return LBM_ERR_ARG;
+  *n_boundary = c->n_slow;
+  return LBM_OK;
+}
+
 int lbm_profile(lbm_ctx* c, int enabled) {
   if (!c) return LBM_ERR_ARG;
-  int rc = harvest_profile(c);
-  if (rc) return rc;
+  RCK(harvest_profile(c));
   c->prof = enabled != 0;
   c->kernel_ms = 0.0;
   c->launches = 0;
+  c->kind_ms[0] = c->kind_ms[1] = 0.0;
+  c->kind_n[0] = c->kind_n[1] = 0;
+  return LBM_OK;
+}
+
+int lbm_kernel_times(lbm_ctx* c, int kind, double* ms, int64_t* launches) {
+  if (!c || kind < 0 || kind > 1) return LBM_ERR_ARG;
+  RCK(harvest_profile(c));
+  if (ms) *ms = c->kind_ms[kind];
+  if (launches) *launches = c->kind_n[kind];
   return LBM_OK;
 }
 
 int lbm_stats(lbm_ctx* c, double* kernel_ms, int64_t* launches, double* algo_bytes) {
   if (!c) return LBM_ERR_ARG;
-  int rc = harvest_profile(c);
-  if (rc) return rc;
+  RCK(harvest_profile(c));
   if (kernel_ms) *kernel_ms = c->kernel_ms;
   if (launches) *launches = c->launches;
   if (algo_bytes) *algo_bytes = 152.0 * (double)c->n_fluid;
@@ -659,30 +762,21 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
 
 namespace {
 __global__ void k_sum_locals(ConvState** convs, int n) {
+  if (convs[0]->stopped) return;
   double s = 0.0;
   for (int i = 0; i < n; ++i) s += convs[i]->s_local;
   for (int i = 0; i < n; ++i) convs[i]->s_global = s;
 }
 
-int copy_plane(lbm_ctx* dst, int bd, int zd, lbm_ctx* src, int bs, int zs, int q, hipStream_t st) {
-  const Layout& L = src->L;
-  HIPCK(src, hipMemcpyAsync(pop(dst, bd, q) + (int64_t)zd * L.plane, pop(src, bs, q) + (int64_t)zs * L.plane,
-                            sizeof(float) * L.plane, hipMemcpyDeviceToDevice, st));
-  return LBM_OK;
-}
-
-// slab i's top plane -> slab i+1's bottom ghost; slab i+1's bottom plane -> slab i's top ghost
+// slab i's packed top face -> slab i+1's bottom ghost; slab i+1's bottom face -> slab i's top
 int loopback_exchange(lbm_ctx** cs, int n, int b, bool all, hipStream_t st) {
+  for (int i = 0; i < n; ++i) RCK(pack_faces(cs[i], b, all, st));
+  const size_t bytes = sizeof(float) * (all ? kQ : 5) * (size_t)cs[0]->L.plane;
   for (int i = 0; i + 1 < n; ++i) {
-    lbm_ctx *a = cs[i], *u = cs[i + 1];
-    for (int k = 0; k < (all ? 19 : 5); ++k) {
-      const int qu = all ? k : kUpSet[k], qd = all ? k : kDownSet[k];
-      int rc = copy_plane(u, b, 0, a, b, a->L.nz, qu, st);
-      if (rc) return rc;
-      rc = copy_plane(a, b, a->L.nz + 1, u, b, 1, qd, st);
-      if (rc) return rc;
-    }
+    HIPCK(cs[i], hipMemcpyAsync(cs[i + 1]->recv_dn, cs[i]->send_up, bytes, hipMemcpyDeviceToDevice, st));
+    HIPCK(cs[i], hipMemcpyAsync(cs[i]->recv_up, cs[i + 1]->send_dn, bytes, hipMemcpyDeviceToDevice, st));
   }
+  for (int i = 0; i < n; ++i) RCK(unpack_faces(cs[i], b, all, i > 0, i + 1 < n, st));
   return LBM_OK;
 }
 }  // namespace
@@ -692,22 +786,23 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   lbm_ctx* c0 = cs[0];
   for (int i = 0; i < n; ++i) {
     if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.ny != c0->L.ny ||
-        cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled)
+        cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled || cs[i]->comm)
       return LBM_ERR_ARG;
   }
   HIPCK(c0, hipSetDevice(c0->d.device));
-  hipStream_t st = c0->s_comp;  // one stream: slabs run back to back (debug / parity path)
-  for (int i = 0; i < n; ++i) HIPCK(c0, hipStreamSynchronize(cs[i]->s_comp));
+  hipStream_t st = c0->s_comp;  // one stream: slabs run back to back (test / debug path)
+  for (int i = 0; i < n; ++i) {
+    HIPCK(c0, hipStreamSynchronize(cs[i]->s_comp));
+    RCK(ensure_halo_buffers(cs[i]));
+  }
   ConvState** dconvs = nullptr;
   HIPCK(c0, hipMalloc(&dconvs, sizeof(ConvState*) * n));
   std::vector<ConvState*> hc(n);
   for (int i = 0; i < n; ++i) hc[i] = cs[i]->conv;
   HIPCK(c0, hipMemcpy(dconvs, hc.data(), sizeof(ConvState*) * n, hipMemcpyHostToDevice));
-  int rc = ensure_hist(c0, std::max(nsteps, 1));
-  if (rc) return rc;
+  RCK(ensure_hist(c0, std::max(nsteps, 1)));
   if (!c0->halo_primed) {
-    rc = loopback_exchange(cs, n, c0->steps_done & 1, true, st);
-    if (rc) return rc;
+    RCK(loopback_exchange(cs, n, c0->steps_done & 1, true, st));
     for (int i = 0; i < n; ++i) cs[i]->halo_primed = true;
   }
   int h = c0->steps_done;
@@ -715,15 +810,12 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     const bool store_all = (s == nsteps - 1);
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      StepArgs a = make_args(c, h, 1, c->L.nz + 1, c->partial, store_all);
-      std::swap(c->s_comp, st);  // launch on the group stream
-      rc = launch_cs(c, a, c->grid_full);
-      std::swap(c->s_comp, st);
-      if (rc) return rc;
-      HIPCK(c, launch_finish(c->partial, c->grid_full, c->conv, nullptr, 0, st));
+      RCK(run_range(c, c->lo, h, store_all, st));
+      if (c->L.nz > 1) RCK(run_range(c, c->hi, h, store_all, st));
+      RCK(run_range(c, c->mid, h, store_all, st));
+      HIPCK(c, launch_reduce(c->lo.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
     }
-    rc = loopback_exchange(cs, n, (h + 1) & 1, false, st);
-    if (rc) return rc;
+    RCK(loopback_exchange(cs, n, (h + 1) & 1, false, st));
     hipLaunchKernelGGL(k_sum_locals, dim3(1), dim3(1), 0, st, dconvs, n);
     for (int i = 0; i < n; ++i)
       HIPCK(c0, launch_finish_global(cs[i]->conv, (i == 0 && residual_hist) ? c0->hist + s : nullptr, st));

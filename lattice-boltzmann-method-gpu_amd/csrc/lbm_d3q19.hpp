@@ -60,7 +60,9 @@ constexpr int face_bits() {
          (Dir<Q>::y == -1 ? 8 : 0) | (Dir<Q>::z == 1 ? 16 : 0) | (Dir<Q>::z == -1 ? 32 : 0);
 }
 
-// Cell-type byte.  bits 0-1 class; fluid: bit 2 slow path, bit 3 keep macros each step;
+// Cell-type byte.  bits 0-1 class; fluid: bit 2 has a wall neighbour (bounce-back patched
+// inline by the stream-collide kernel from a per-cell link mask), bit 3 has an NEE neighbour
+// (the cell is re-done by the boundary fix-up kernel, which keeps its previous (rho, u));
 // NEE boundary cell: bits 4-6 face, bit 7 kind (0 velocity, 1 pressure).
 enum : uint8_t {
   kPassive = 0,   // ghost / unused / padding: never updated, pulled raw (constant)
@@ -68,8 +70,8 @@ enum : uint8_t {
   kNee = 2,       // non-equilibrium extrapolation boundary cell
   kFluid = 3,     // collide + stream
   kClassMask = 3,
-  kSlow = 1u << 2,      // fluid with a wall or NEE neighbour
-  kNeedsMac = 1u << 3,  // fluid with an NEE neighbour: its own (rho,u) is stored every step
+  kWallAdj = 1u << 2,   // fluid with a wall neighbour
+  kNeedsMac = 1u << 3,  // fluid with an NEE neighbour
   kKindPressure = 1u << 7,
 };
 LBM_HD int nee_face(uint8_t t) { return (t >> 4) & 7; }

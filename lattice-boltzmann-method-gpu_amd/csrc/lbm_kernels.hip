@@ -1,27 +1,37 @@
 // lbm_kernels.hip -- CDNA4 (gfx950) kernels of the D3Q19 BGK hot path.
 //
-// One fused kernel replaces the reference's update + boundary_stream + calc_vel_square
-// (ldc.cu:57-466, Poiseulle.cu:384-901, bifurcation.cu:429-1023):
-//   * pull streaming from the SoA source buffer (19 coalesced 256-B wavefront loads);
-//   * boundaries are evaluated on the CONSUMER side, selected by the neighbour's type
-//     byte: a fluid cell F that would pull population q from
-//       - a wall W: takes src[opp q][F] (half-way bounce-back, ldc.cu:184-201 /
-//         Poiseulle.cu:601-746 write exactly this value into W one pass earlier);
-//       - an NEE cell B with e_q . n_B = 1: takes
-//           feq_q(rho_bc, u_bc) + (src[q][F] - feq_q(rho_F, u_F)) * (1 - 1/tau)
-//         with F's own (rho,u) of the previous step -- the value boundary_stream
-//         writes into B (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021;
-//         their hand-simplified "tmp" terms are bit-identical to feq_q(rho_bc, u_bc));
-//     so no boundary pass, no boundary-cell writes and no second launch are needed;
-//   * moments, BGK relaxation and the |u| partial sum of the residual in registers.
-// HBM traffic per fluid cell: 76 B loaded + 76 B stored + 1 B type (+16 B macros on the
-// last step of a call and for cells next to an NEE boundary).
+// The reference's per-step kernels update + boundary_stream + calc_vel_square
+// (ldc.cu:57-466, Poiseulle.cu:384-901, bifurcation.cu:429-1023) become:
+//
+//  k_stream_collide  one wavefront per 256-cell AoSoA chunk, 4 consecutive cells per
+//                    lane: 19 aligned 16-B pulls (x neighbours by a DPP lane shift, the two
+//                    edge lanes read one extra float), moments, equilibria and BGK
+//                    relaxation in registers, 19 16-B stores into the chunk.
+//                    Boundaries are evaluated on the CONSUMER side: a population pulled
+//                    from a wall W at c - e_q is replaced, in the lanes holding wall-
+//                    adjacent cells only, by f_q = src[opp q][c] (half-way bounce-back:
+//                    the value Poiseulle.cu:601-746 / ldc.cu:184-201 put into W one pass
+//                    earlier), selected by a per-cell wall-link bit mask.
+//  k_boundary_fixup  one thread per fluid cell next to an NEE cell (a compact list of
+//                    contiguous rows, ~0.2% of the cells at 512^3): re-does the cell and
+//                    overwrites it, with
+//                      NEE cell B at c - e_q with e_q . n_B = 1:
+//                        f_q = feq_q(rho_bc, u_bc) + (src[q][c] - feq_q(rho_c, u_c)) (1 - 1/tau)
+//                        with the cell's own (rho, u) of the previous step (the value
+//                        boundary_stream writes into B, ldc.cu:391-456, Poiseulle.cu:748-891,
+//                        bifurcation.cu:877-1021; their hand-simplified "tmp" terms are
+//                        bit-identical to feq_q(rho_bc, u_bc)).
+//  k_reduce_*        deterministic two-level sum of the per-block |u| partials and the
+//                    residual / convergence logic of ldc.cu:660-684 on the device.
+// HBM traffic per fluid cell: 76 B loaded + 76 B stored + 1 B type.
 #include "lbm_d3q19.hpp"
 #include "lbm_kernels.hpp"
 
 namespace lbm {
 
 namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -41,37 +51,157 @@ __device__ __forceinline__ double block_sum(double v, double* lds) {
   return s;
 }
 
-struct Pop {
-  float v[19];
-};
+// DPP whole-wave lane shifts (gfx9 wave_shr:1 / wave_shl:1)
+__device__ __forceinline__ float lane_from_prev(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_from_next(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, false));
+}
 
-// Raw pull of population Q from c - e_Q.
 template <int Q>
-__device__ __forceinline__ void pull(Pop& f, const float* __restrict__ src, int64_t qs, int c,
-                                     int pitch, int64_t plane) {
-  const int off = Dir<Q>::x + Dir<Q>::y * pitch + Dir<Q>::z * (int)plane;
-  f.v[Q] = src[Q * qs + (c - off)];
+constexpr int64_t row_off(int pitch, int64_t plane) {
+  return Dir<Q>::y * (int64_t)pitch + Dir<Q>::z * plane;
+}
+
+// population Q of the lane's 4 cells c..c+3, pulled from c - e_Q .. c+3 - e_Q
+template <int Q>
+__device__ __forceinline__ f4 pull4(const float* __restrict__ src, int64_t c, int lane, int pitch, int64_t plane) {
+  const int64_t b = c - row_off<Q>(pitch, plane);
+  const f4 a = *reinterpret_cast<const f4*>(src + aidx(b, Q));
+  if constexpr (Dir<Q>::x == 0) {
+    return a;
+  } else if constexpr (Dir<Q>::x == 1) {  // needs b-1 .. b+2
+    float p = lane_from_prev(a.w);
+    if (lane == 0) p = src[aidx(b - 1, Q)];
+    return f4{p, a.x, a.y, a.z};
+  } else {                                 // needs b+1 .. b+4
+    float n = lane_from_next(a.x);
+    if (lane == 63) n = src[aidx(b + 4, Q)];
+    return f4{a.y, a.z, a.w, n};
+  }
 }
 
 template <int... Qs>
-__device__ __forceinline__ void pull_all(Pop& f, const float* __restrict__ src, int64_t qs, int c,
-                                         int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
-  (pull<Qs>(f, src, qs, c, pitch, plane), ...);
+__device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t c, int lane, int pitch,
+                                          int64_t plane, std::integer_sequence<int, Qs...>) {
+  ((v[Qs] = pull4<Qs>(src, c, lane, pitch, plane)), ...);
 }
+
+template <int J, int... Qs>
+__device__ __forceinline__ void relax4(f4* v, float tau, float r, float ux, float uy, float uz,
+                                       std::integer_sequence<int, Qs...>) {
+  ((v[Qs][J] = v[Qs][J] - (v[Qs][J] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
+}
+
+using AllQ = std::make_integer_sequence<int, kQ>;
+
+// half-way bounce-back for cell J of the lane: a population pulled from a wall is replaced by
+// the cell's own opposite population (the value Poiseulle.cu:601-746 / ldc.cu:184-201 store in
+// the wall one pass earlier)
+template <int J, int Q>
+__device__ __forceinline__ void bb_one(f4* v, const float* __restrict__ src, int64_t c, uint32_t m) {
+  if constexpr (Q > 0) {
+    if (m & (1u << Q)) v[Q][J] = src[aidx(c + J, Dir<Q>::opp)];
+  }
+}
+template <int J, int... Qs>
+__device__ __forceinline__ void bb_cell(f4* v, const float* __restrict__ src, int64_t c, uint32_t m,
+                                        std::integer_sequence<int, Qs...>) {
+  (bb_one<J, Qs>(v, src, c, m), ...);
+}
+
+// moments (ldc.cu:316-322): sequential fp32 sum; signed sums in the reference order
+template <int J>
+__device__ __forceinline__ void collide_cell(f4* v, float tau, float& rho, float& ux, float& uy, float& uz) {
+  float r = 0.f;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) r = r + v[q][J];
+  ux = (v[1][J] - v[2][J] + v[7][J] + v[8][J] - v[9][J] - v[10][J] + v[11][J] + v[12][J] - v[13][J] - v[14][J]) / r;
+  uy = (v[3][J] - v[4][J] + v[7][J] - v[8][J] + v[9][J] - v[10][J] + v[15][J] - v[16][J] + v[17][J] - v[18][J]) / r;
+  uz = (v[5][J] - v[6][J] + v[11][J] - v[12][J] + v[13][J] - v[14][J] + v[15][J] + v[16][J] - v[17][J] - v[18][J]) / r;
+  rho = r;
+  relax4<J>(v, tau, r, ux, uy, uz, AllQ{});
+}
+
+__global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
+  __shared__ double red[kBlock / 64];
+  if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int idx = blockIdx.x * (kBlock / 64) + wave;
+  double acc = 0.0;
+  if (idx < a.nchunks) {
+    const int64_t ch = a.chunks[idx];
+    const int64_t c = ch * kChunk + lane * 4;
+    f4 v[kQ];
+    pull4_all(v, a.src, c, lane, a.pitch, a.plane, AllQ{});
+    const unsigned t4 = *reinterpret_cast<const unsigned*>(a.type + c);
+    constexpr unsigned kWall4 = kWallAdj * 0x01010101u;
+    if (a.bb_active && (t4 & kWall4)) {  // rare, divergent: lanes holding wall-adjacent cells
+      if (t4 & (kWallAdj << 0)) bb_cell<0>(v, a.src, c, a.links[c + 0], AllQ{});
+      if (t4 & (kWallAdj << 8)) bb_cell<1>(v, a.src, c, a.links[c + 1], AllQ{});
+      if (t4 & (kWallAdj << 16)) bb_cell<2>(v, a.src, c, a.links[c + 2], AllQ{});
+      if (t4 & (kWallAdj << 24)) bb_cell<3>(v, a.src, c, a.links[c + 3], AllQ{});
+    }
+    float r0, r1, r2, r3, x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
+    collide_cell<0>(v, a.tau, r0, x0, y0, z0);
+    collide_cell<1>(v, a.tau, r1, x1, y1, z1);
+    collide_cell<2>(v, a.tau, r2, x2, y2, z2);
+    collide_cell<3>(v, a.tau, r3, x3, y3, z3);
+    const f4 R{r0, r1, r2, r3}, UX{x0, x1, x2, x3}, UY{y0, y1, y2, y3}, UZ{z0, z1, z2, z3};
+    unsigned store = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned t = (t4 >> (8 * j)) & 0xffu;
+      const int64_t cj = c + j;
+      const bool in = cj >= a.c_lo && cj < a.c_hi && (t & kClassMask) == kFluid;
+      if (in) {
+        store |= 1u << j;
+        if (!(t & kNeedsMac)) acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
+      }
+    }
+    float* d = a.dst + aidx(c, 0);
+    if (store == 0xfu) {
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));
+      if (a.store_all_macros) {
+        *reinterpret_cast<f4*>(a.rho + c) = R;
+        *reinterpret_cast<f4*>(a.ux + c) = UX;
+        *reinterpret_cast<f4*>(a.uy + c) = UY;
+        *reinterpret_cast<f4*>(a.uz + c) = UZ;
+      }
+    } else if (store) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!(store & (1u << j))) continue;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) d[q * kChunk + j] = v[q][j];
+        if (a.store_all_macros) {
+          a.rho[c + j] = R[j]; a.ux[c + j] = UX[j]; a.uy[c + j] = UY[j]; a.uz[c + j] = UZ[j];
+        }
+      }
+    }
+  }
+  const double s = block_sum(acc, red);
+  if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
+}
+
+// ---- boundary fix-up ------------------------------------------------------------------
 
 struct Macro {
   float rho, ux, uy, uz;
 };
 
-// Boundary patch of population Q for a slow-path cell (neighbour is a wall or NEE cell).
 template <int Q>
-__device__ __forceinline__ void patch(Pop& f, const StepArgs& a, int c, const Macro& mp) {
-  const int off = Dir<Q>::x + Dir<Q>::y * a.pitch + Dir<Q>::z * (int)a.plane;
-  const int nb = c - off;
+__device__ __forceinline__ void fix_pull(float* f, const FixArgs& a, int64_t c, const Macro& mp) {
+  const int64_t nb = c - (Dir<Q>::x + row_off<Q>(a.pitch, a.plane));
+  f[Q] = a.src[aidx(nb, Q)];
+  if constexpr (Q == 0) return;
   const uint8_t tn = a.type[nb];
   const int cls = tn & kClassMask;
   if (cls == kWall) {
-    if (a.bb_active) f.v[Q] = a.src[Dir<Q>::opp * a.qstride + c];
+    if (a.bb_active) f[Q] = a.src[aidx(c, Dir<Q>::opp)];
   } else if (cls == kNee) {
     if (a.nee_active && ((face_bits<Q>() >> nee_face(tn)) & 1)) {
       float rb, bx, by, bz;
@@ -82,78 +212,55 @@ __device__ __forceinline__ void patch(Pop& f, const StepArgs& a, int c, const Ma
         rb = mp.rho;
         bx = a.ux[nb]; by = a.uy[nb]; bz = a.uz[nb];
       }
-      const float own = a.src[Q * a.qstride + c];
+      const float own = a.src[aidx(c, Q)];
       const float e_bc = feq<Q>(rb, bx, by, bz);
       const float e_nb = feq<Q>(mp.rho, mp.ux, mp.uy, mp.uz);
-      f.v[Q] = e_bc + (own - e_nb) * a.omc;
+      f[Q] = e_bc + (own - e_nb) * a.omc;
     }
   }
 }
 
 template <int... Qs>
-__device__ __forceinline__ void patch_all(Pop& f, const StepArgs& a, int c, const Macro& mp,
-                                          std::integer_sequence<int, Qs...>) {
-  (patch<Qs>(f, a, c, mp), ...);
-}
-
-template <int Q>
-__device__ __forceinline__ void relax_store(const Pop& f, float* __restrict__ dst, int64_t qs, int c,
-                                            float tau, float r, float ux, float uy, float uz) {
-  const float e = feq<Q>(r, ux, uy, uz);
-  dst[Q * qs + c] = f.v[Q] - (f.v[Q] - e) / tau;
+__device__ __forceinline__ void fix_pull_all(float* f, const FixArgs& a, int64_t c, const Macro& mp,
+                                             std::integer_sequence<int, Qs...>) {
+  (fix_pull<Qs>(f, a, c, mp), ...);
 }
 
 template <int... Qs>
-__device__ __forceinline__ void relax_all(const Pop& f, float* __restrict__ dst, int64_t qs, int c,
-                                          float tau, float r, float ux, float uy, float uz,
-                                          std::integer_sequence<int, Qs...>) {
-  (relax_store<Qs>(f, dst, qs, c, tau, r, ux, uy, uz), ...);
+__device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, float tau, float r,
+                                              float ux, float uy, float uz, std::integer_sequence<int, Qs...>) {
+  ((dst[aidx(c, Qs)] = f[Qs] - (f[Qs] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
 }
 
-using AllQ = std::make_integer_sequence<int, 19>;
-
-__global__ __launch_bounds__(kBlock) void k_collide_stream(const StepArgs a) {
-  __shared__ double red[kBlock / 64];
-  if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, step is a no-op
-  const int lane = threadIdx.x & 63;
-  const int row = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void k_boundary_fixup(const FixArgs a) {
+  __shared__ double red[4];
+  if (a.stopped != nullptr && *a.stopped) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   double acc = 0.0;
-  for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-    const int txi = t % a.ntx;
-    const int r = t / a.ntx;
-    const int tyi = r % a.nty;
-    const int z = a.z_begin + r / a.nty;
-    const int x = txi * kTileX + lane;
-    const int y = tyi * kTileY + row;
-    if (y >= a.ny) continue;
-    const int c = x + y * a.pitch + z * (int)a.plane;
-    const uint8_t tc = a.type[c];
-    if ((tc & kClassMask) != kFluid) continue;
-
-    Pop f;
-    pull_all(f, a.src, a.qstride, c, a.pitch, a.plane, AllQ{});
-    if (tc & kSlow) {
-      Macro mp{0.f, 0.f, 0.f, 0.f};
-      if (tc & kNeedsMac) mp = Macro{a.rho[c], a.ux[c], a.uy[c], a.uz[c]};
-      patch_all(f, a, c, mp, AllQ{});
-    }
-    // moments (ldc.cu:316-322): sequential fp32 sum, signed sums in reference order
+  if (i < a.n) {
+    const int64_t c = a.cells[i];
+    const float4 pv = a.prev[i];
+    const Macro mp{pv.x, pv.y, pv.z, pv.w};
+    float f[kQ];
+    fix_pull_all(f, a, c, mp, AllQ{});
     float rho = 0.f;
 #pragma unroll
-    for (int q = 0; q < 19; ++q) rho = rho + f.v[q];
-    const float* v = f.v;
-    const float ux = (v[1] - v[2] + v[7] + v[8] - v[9] - v[10] + v[11] + v[12] - v[13] - v[14]) / rho;
-    const float uy = (v[3] - v[4] + v[7] - v[8] + v[9] - v[10] + v[15] - v[16] + v[17] - v[18]) / rho;
-    const float uz = (v[5] - v[6] + v[11] - v[12] + v[13] - v[14] + v[15] + v[16] - v[17] - v[18]) / rho;
-    if (a.store_all_macros || (tc & kNeedsMac)) {
+    for (int q = 0; q < kQ; ++q) rho = rho + f[q];
+    const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
+    const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
+    const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
+    fix_store_all(f, a.dst, c, a.tau, rho, ux, uy, uz, AllQ{});
+    a.prev[i] = make_float4(rho, ux, uy, uz);
+    if (a.store_all_macros) {
       a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
     }
-    relax_all(f, a.dst, a.qstride, c, a.tau, rho, ux, uy, uz, AllQ{});
-    acc += (double)sqrtf(ux * ux + uy * uy + uz * uz);
+    acc = (double)sqrtf(ux * ux + uy * uy + uz * uz);
   }
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
 }
+
+// ---- residual --------------------------------------------------------------------------
 
 __device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
   // ldc.cu:662-684: residual = |S_k - S_{k-1}| / S_k on fp32 sums
@@ -167,12 +274,23 @@ __device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
   if (hist_slot) *hist_slot = residual;
 }
 
-__global__ __launch_bounds__(256) void k_finish(const double* __restrict__ partial, int n,
-                                                ConvState* cv, float* hist_slot, int finish) {
+__global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict__ partial, int n,
+                                                       double* __restrict__ out, const ConvState* cv) {
   __shared__ double red[4];
   if (cv->stopped) return;
+  const int len = (n + gridDim.x - 1) / gridDim.x;
+  const int lo = blockIdx.x * len, hi = min(n, lo + len);
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s += partial[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__ slices, int n, ConvState* cv,
+                                                      float* hist_slot, int finish) {
+  __shared__ double red[4];
+  if (cv->stopped) return;
+  double s = threadIdx.x < n ? slices[threadIdx.x] : 0.0;
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
     cv->s_local = s;
@@ -185,12 +303,33 @@ __global__ void k_finish_global(ConvState* cv, float* hist_slot) {
   residual_logic(cv, cv->s_global, hist_slot);
 }
 
+// ---- halo pack / unpack ----------------------------------------------------------------
+
+__global__ void k_pack(const float* __restrict__ f, float* __restrict__ buf, int zs, int64_t plane,
+                       const int* __restrict__ qs, int nq) {
+  const int64_t n = plane * nq;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / plane);
+    const int64_t c = (int64_t)zs * plane + (i - k * plane);
+    buf[i] = f[aidx(c, qs[k])];
+  }
+}
+
+__global__ void k_unpack(float* __restrict__ f, const float* __restrict__ buf, int zs, int64_t plane,
+                         const int* __restrict__ qs, int nq) {
+  const int64_t n = plane * nq;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / plane);
+    const int64_t c = (int64_t)zs * plane + (i - k * plane);
+    f[aidx(c, qs[k])] = buf[i];
+  }
+}
+
 // ---- geometry --------------------------------------------------------------------------
 
-// reference code -> class/face/kind, NEE data into the macro arrays of NEE cells
+// reference code -> class/face/kind; NEE data into the macro arrays of NEE cells
 __global__ void k_classify(const GeoArgs g) {
-  const int64_t n = g.plane * g.planes;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int code = g.codes[c];
     const int x = (int)(c % g.pitch);
@@ -201,23 +340,22 @@ __global__ void k_classify(const GeoArgs g) {
       if (g.case_kind == 0) {  // LDC (ldc.cu:469): 0 ghost, 1 wall, 2 lid, 3 fluid
         if (code == 1) t = kWall;
         else if (code == 3) t = kFluid;
-        else if (code == 2) {
-          t = make_nee(kFaceNY, false);  // lid supplies {4,8,10,16,18} (ldc.cu:391-456)
+        else if (code == 2) {  // lid supplies {4,8,10,16,18} (ldc.cu:391-456), u = (0, 0, u_lid)
+          t = make_nee(kFaceNY, false);
           g.rho[c] = 0.f; g.ux[c] = 0.f; g.uy[c] = 0.f; g.uz[c] = g.lid_u;
         }
       } else {  // Poiseuille / mask (README.md:9-14)
+        const bool in_tab = zg >= 0 && zg < g.nz_global;
         if (code == 1) t = kWall;
         else if (code == 4) t = kFluid;
-        else if (code == 2) {   // inlet, +y face {3,7,9,15,17}, u = (0, inlet_uy(x,z), 0)
+        else if (code == 2) {   // inlet: +y face {3,7,9,15,17}, u = (0, inlet_uy(x,z), 0)
           t = make_nee(kFacePY, false);
-          const bool in_tab = g.inlet_uy && zg >= 0 && zg < g.nz_global;
-          const float u = in_tab ? g.inlet_uy[x + (int64_t)zg * g.nx] : 0.f;
+          const float u = (g.inlet_uy && in_tab) ? g.inlet_uy[x + (int64_t)zg * g.nx] : 0.f;
           g.rho[c] = 0.f; g.ux[c] = 0.f; g.uy[c] = u; g.uz[c] = 0.f;
-        } else if (code == 3) { // outlet, -y face {4,8,10,16,18}
+        } else if (code == 3) { // outlet: -y face {4,8,10,16,18}
           if (g.case_kind == 1) {  // Poiseuille: velocity, u = (0, outlet_uy(x,z), 0)
             t = make_nee(kFaceNY, false);
-            const bool in_tab = g.outlet_uy && zg >= 0 && zg < g.nz_global;
-            const float u = in_tab ? g.outlet_uy[x + (int64_t)zg * g.nx] : 0.f;
+            const float u = (g.outlet_uy && in_tab) ? g.outlet_uy[x + (int64_t)zg * g.nx] : 0.f;
             g.rho[c] = 0.f; g.ux[c] = 0.f; g.uy[c] = u; g.uz[c] = 0.f;
           } else {                 // bifurcation: pressure, rho = 1 (bifurcation.cu:890)
             t = make_nee(kFaceNY, true);
@@ -231,38 +369,41 @@ __global__ void k_classify(const GeoArgs g) {
 }
 
 template <int Q>
-__device__ __forceinline__ void scan_nb(const uint8_t* type, int64_t c, int pitch, int64_t plane,
-                                        int64_t n, uint8_t& flags) {
-  const int64_t nb = c - (Dir<Q>::x + Dir<Q>::y * (int64_t)pitch + Dir<Q>::z * plane);
-  if (nb < 0 || nb >= n) return;
+__device__ __forceinline__ void scan_nb(const uint8_t* type, int64_t c, const GeoArgs& g, uint8_t& flags,
+                                        uint32_t& walls) {
+  const int64_t nb = c - (Dir<Q>::x + Dir<Q>::y * (int64_t)g.pitch + Dir<Q>::z * g.plane);
+  if (Q == 0 || nb < 0 || nb >= g.ncell) return;
   const uint8_t tn = type[nb];
   const int cls = tn & kClassMask;
-  if (cls == kWall) flags |= kSlow;
-  if (cls == kNee && ((face_bits<Q>() >> nee_face(tn)) & 1)) flags |= kSlow | kNeedsMac;
+  if (cls == kWall) {
+    flags |= kWallAdj;
+    walls |= 1u << Q;
+  }
+  if (cls == kNee && ((face_bits<Q>() >> nee_face(tn)) & 1)) flags |= kNeedsMac;
 }
 
 template <int... Qs>
-__device__ __forceinline__ void scan_all(const uint8_t* type, int64_t c, int pitch, int64_t plane,
-                                         int64_t n, uint8_t& flags, std::integer_sequence<int, Qs...>) {
-  (scan_nb<Qs>(type, c, pitch, plane, n, flags), ...);
+__device__ __forceinline__ void scan_all(const uint8_t* type, int64_t c, const GeoArgs& g, uint8_t& flags,
+                                         uint32_t& walls, std::integer_sequence<int, Qs...>) {
+  (scan_nb<Qs>(type, c, g, flags, walls), ...);
 }
 
 __global__ void k_flag_fluid(const GeoArgs g) {
-  const int64_t n = g.plane * g.planes;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
     const uint8_t t = g.type[c];
     if ((t & kClassMask) != kFluid) continue;
     uint8_t flags = 0;
-    scan_all(g.type, c, g.pitch, g.plane, n, flags, AllQ{});
+    uint32_t walls = 0;
+    scan_all(g.type, c, g, flags, walls, AllQ{});
     g.type[c] = (uint8_t)(t | flags);
+    g.links[c] = walls;
   }
 }
 
-__global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int planes, int64_t plane,
-                            int z_offset, int nzg) {
-  const int64_t n = plane * planes;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n;
+__global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int64_t plane, int64_t ncell, int z_offset,
+                            int nzg) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int x = (int)(c % pitch);
     const int y = (int)((c / pitch) % ny);
@@ -279,33 +420,28 @@ __global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int planes
 
 // ---- initial state ---------------------------------------------------------------------
 
-__global__ void k_init_feq(float* fa, float* fb, int64_t qs, int64_t n, int form,
-                           const float* rho, const float* ux, const float* uy, const float* uz) {
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n;
-       c += (int64_t)gridDim.x * blockDim.x) {
+__global__ void k_init_feq(float* fa, float* fb, int64_t n, int form, const float* rho, const float* ux,
+                           const float* uy, const float* uz) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
     const float r = rho ? rho[c] : 1.0f;
     const float vx = ux ? ux[c] : 0.0f, vy = uy ? uy[c] : 0.0f, vz = uz ? uz[c] : 0.0f;
-    float e[19];
+    float e[kQ];
     if (form == 0) feq_init_wi(r, vx, vy, vz, e);
     else feq_expanded(r, vx, vy, vz, e);
 #pragma unroll
-    for (int q = 0; q < 19; ++q) { fa[q * qs + c] = e[q]; fb[q * qs + c] = e[q]; }
+    for (int q = 0; q < kQ; ++q) { fa[aidx(c, q)] = e[q]; fb[aidx(c, q)] = e[q]; }
   }
 }
 
-__global__ void k_init_ldc(float* fa, float* fb, int64_t qs, int nx, int ny, int pitch, int planes,
-                           int64_t plane, int z_offset, float lid_u) {
-  const int64_t n = plane * planes;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n;
-       c += (int64_t)gridDim.x * blockDim.x) {
+__global__ void k_init_ldc(float* fa, float* fb, int64_t n, int pitch, int ny, float lid_u) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
     const int y = (int)((c / pitch) % ny);
-    (void)nx; (void)z_offset;
     // ldc.cu:510-532: rho 1, u 0; uz = u_max on y = ny-1 and y = ny-2
     const float uz = (y == ny - 1 || y == ny - 2) ? lid_u : 0.0f;
-    float e[19];
+    float e[kQ];
     feq_init_wi(1.0f, 0.0f, 0.0f, uz, e);
 #pragma unroll
-    for (int q = 0; q < 19; ++q) { fa[q * qs + c] = e[q]; fb[q * qs + c] = e[q]; }
+    for (int q = 0; q < kQ; ++q) { fa[aidx(c, q)] = e[q]; fb[aidx(c, q)] = e[q]; }
   }
 }
 
@@ -318,14 +454,23 @@ int grid_for(int64_t n, int block) {
 
 }  // namespace
 
-hipError_t launch_collide_stream(const StepArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_collide_stream, dim3(grid), dim3(kBlock), 0, s, a);
+int main_grid(int nchunks) { return std::max(1, (nchunks + kBlock / 64 - 1) / (kBlock / 64)); }
+int fix_grid(int n) { return std::max(1, (n + 255) / 256); }
+
+hipError_t launch_main(const MainArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_stream_collide, dim3(main_grid(a.nchunks)), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_finish(const double* partial, int n, ConvState* conv, float* hist_slot, int finish,
+hipError_t launch_fix(const FixArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_boundary_fixup, dim3(fix_grid(a.n)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot, int finish,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(256), 0, s, partial, n, conv, hist_slot, finish);
+  hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, kReduceBlocks, conv, hist_slot, finish);
   return hipGetLastError();
 }
 
@@ -334,34 +479,41 @@ hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s
   return hipGetLastError();
 }
 
+hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const int* qs, int nq, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack, dim3(grid_for(plane * nq, 256)), dim3(256), 0, s, f, buf, zs, plane, qs, nq);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack(float* f, const float* buf, int zs, int64_t plane, const int* qs, int nq, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack, dim3(grid_for(plane * nq, 256)), dim3(256), 0, s, f, buf, zs, plane, qs, nq);
+  return hipGetLastError();
+}
+
 hipError_t launch_classify(const GeoArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_classify, dim3(grid_for(g.plane * g.planes, 256)), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_classify, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_flag_fluid, dim3(grid_for(g.plane * g.planes, 256)), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_flag_fluid, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
-hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int planes, int64_t plane,
-                            int z_offset, int nz_global, hipStream_t s) {
-  hipLaunchKernelGGL(k_ldc_codes, dim3(grid_for(plane * planes, 256)), dim3(256), 0, s, codes, nx, ny,
-                     pitch, planes, plane, z_offset, nz_global);
+hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int64_t plane, int64_t ncell, int z_offset,
+                            int nz_global, hipStream_t s) {
+  hipLaunchKernelGGL(k_ldc_codes, dim3(grid_for(ncell, 256)), dim3(256), 0, s, codes, nx, ny, pitch, plane, ncell,
+                     z_offset, nz_global);
   return hipGetLastError();
 }
 
-hipError_t launch_init_feq(float* fa, float* fb, int64_t qstride, int64_t n, int form, const float* rho,
-                           const float* ux, const float* uy, const float* uz, hipStream_t s) {
-  hipLaunchKernelGGL(k_init_feq, dim3(grid_for(n, 256)), dim3(256), 0, s, fa, fb, qstride, n, form, rho,
-                     ux, uy, uz);
+hipError_t launch_init_feq(float* fa, float* fb, int64_t n, int form, const float* rho, const float* ux,
+                           const float* uy, const float* uz, hipStream_t s) {
+  hipLaunchKernelGGL(k_init_feq, dim3(grid_for(n, 256)), dim3(256), 0, s, fa, fb, n, form, rho, ux, uy, uz);
   return hipGetLastError();
 }
 
-hipError_t launch_init_ldc(float* fa, float* fb, int64_t qstride, int nx, int ny, int pitch, int planes,
-                           int64_t plane, int z_offset, float lid_u, hipStream_t s) {
-  hipLaunchKernelGGL(k_init_ldc, dim3(grid_for(plane * planes, 256)), dim3(256), 0, s, fa, fb, qstride,
-                     nx, ny, pitch, planes, plane, z_offset, lid_u);
+hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int ny, float lid_u, hipStream_t s) {
+  hipLaunchKernelGGL(k_init_ldc, dim3(grid_for(n, 256)), dim3(256), 0, s, fa, fb, n, pitch, ny, lid_u);
   return hipGetLastError();
 }
 

@@ -3,43 +3,73 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
 #include <utility>
 
 namespace lbm {
 
-// Device storage of one lattice (or z-slab): raster SoA, x fastest, rows padded to a
-// multiple of 64 floats (one wavefront = one 256-B aligned row segment), one ghost
-// plane below and above the nz local planes (storage plane = local z + 1).
+// Cells are numbered linearly over a padded box, x fastest: c = x + y*pitch + zs*plane
+// with storage plane zs = local z + 1 (one ghost plane below and above the slab).
+// Populations live in AoSoA chunks of 256 consecutive cells -- one wavefront's work
+// (64 lanes x 4 cells): [chunk][q][256].  A wave's 19 loads then fall in a handful of
+// 19-KB chunk blocks instead of 19 streams 0.5 GB apart, and its 19 stores into one.
+constexpr int kChunk = 256;
+constexpr int kQ = 19;
+constexpr int kBlock = 256;  // 4 wavefronts, one chunk each
+
+__host__ __device__ __forceinline__ int64_t aidx(int64_t c, int q) {
+  return ((c >> 8) * kQ + q) * kChunk + (c & (kChunk - 1));
+}
+
 struct Layout {
   int nx, ny, nz;
-  int pitch;        // row pitch in floats (multiple of 64)
-  int planes;       // nz + 2
-  int64_t plane;    // pitch * ny
-  int64_t qstride;  // floats between two populations (>= plane * planes, multiple of 64)
+  int pitch;          // multiple of 4
+  int planes;         // nz + 2
+  int64_t plane;      // pitch * ny
+  int64_t ncell;      // plane * planes rounded up to a whole chunk
+  int64_t nchunk;     // ncell / 256
+  int64_t guard;      // guard chunks before and after the cells (>= one plane + one row + 1)
+  // population buffers: guard + nchunk + guard chunks; the base pointer skips the leading
+  // guard, so the pulls of lanes masked out at the range ends never leave the allocation
+  int64_t buf_floats() const { return (nchunk + 2 * guard) * kQ * kChunk; }
 };
 
-// Arguments of one collide-stream launch over storage planes [z_begin, z_end).
-struct StepArgs {
+// Fused pull-stream + BGK collide over a list of chunks, treating every neighbour as a
+// plain pull; stores fluid cells; |u| partials of fluid cells that are not slow.
+struct MainArgs {
+  const float* src;     // base (past the guard chunk)
+  float* dst;
+  const uint8_t* type;  // per cell
+  const uint32_t* links;  // per cell: bit q set when c - e_q is a wall (read for kWallAdj cells)
+  float* rho; float* ux; float* uy; float* uz;
+  double* partial;      // one per block
+  const int* chunks;    // active chunk ids
+  int nchunks;
+  int pitch;
+  int64_t plane;
+  int64_t c_lo, c_hi;   // cell range of this launch (cells outside are not touched)
+  float tau;
+  int bb_active;        // wall neighbours bounce back (else raw pull: reference step 0)
+  int store_all_macros;
+  const int* stopped;   // nullable
+};
+
+// NEE-adjacent fluid cells, one per thread: wall bounce-back and NEE by mask,
+// overwriting what the main kernel stored for them.
+struct FixArgs {
   const float* src;
   float* dst;
   const uint8_t* type;
-  float* rho;
-  float* ux;
-  float* uy;
-  float* uz;
-  double* partial;      // one |u| partial sum per block
-  int64_t qstride;
+  float* rho; float* ux; float* uy; float* uz;  // full fields; NEE data sits at NEE cells
+  float4* prev;         // per slow cell: its (rho, ux, uy, uz) of the previous step
+  const int* cells;     // slow cell ids (linear)
+  int n;
+  int pitch;
   int64_t plane;
-  int pitch, ny;
-  int z_begin;          // first storage plane
-  int ntx, nty;         // tiles of 64 x 4 cells per plane
-  int ntiles;           // ntx * nty * (z_end - z_begin)
-  float tau;            // BGK: f - (f - feq) / tau
-  float omc;            // (1.0f - 1.0f / tau) of the NEE formula
-  int bb_active;        // wall neighbours bounce back (else raw pull: reference step 0)
-  int nee_active;       // NEE neighbours extrapolate (else raw pull: reference step 0)
-  int store_all_macros; // write (rho,u) of every fluid cell (else only kNeedsMac cells)
-  const int* stopped;   // device convergence flag (nullable)
+  float tau, omc;
+  int bb_active, nee_active, store_all_macros;
+  double* partial;
+  const int* stopped;
 };
 
 struct ConvState {      // device-resident reference main-loop state (ldc.cu:613-685)
@@ -56,43 +86,47 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
   int pad;
 };
 
-constexpr int kBlock = 256;       // 4 wavefronts: 64 x-cells x 4 rows
-constexpr int kTileX = 64, kTileY = 4;
-
-hipError_t launch_collide_stream(const StepArgs& a, int grid, hipStream_t s);
-// sums `n` block partials into conv->s_local; with finish=1 also runs the residual logic
-hipError_t launch_finish(const double* partial, int n, ConvState* conv, float* hist_slot,
+hipError_t launch_main(const MainArgs& a, hipStream_t s);
+hipError_t launch_fix(const FixArgs& a, hipStream_t s);
+int main_grid(int nchunks);
+int fix_grid(int n);
+constexpr int kReduceBlocks = 256;
+// partial sums -> conv->s_local (deterministic two-level tree: kReduceBlocks blocks sum
+// fixed contiguous slices into scratch, one block sums scratch); finish=1 also runs the
+// residual logic and writes *hist_slot
+hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot,
                          int finish, hipStream_t s);
-// residual logic on conv->s_global (multi-rank, after the all-reduce)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
 
-// geometry: reference codes (int8, storage layout incl. ghost planes) -> cell-type bytes
+// halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack
+hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const int* qs_dev, int nq,
+                       hipStream_t s);
+hipError_t launch_unpack(float* f, const float* buf, int zs, int64_t plane, const int* qs_dev, int nq,
+                         hipStream_t s);
+
+// geometry: reference codes (int8 per linear cell) -> cell-type bytes
 struct GeoArgs {
-  const int8_t* codes;  // storage layout, pitch/planes as Layout; padding = 0
+  const int8_t* codes;
   uint8_t* type;
+  uint32_t* links;         // per cell wall-link masks (written for fluid cells)
   float* rho; float* ux; float* uy; float* uz;  // NEE data written at NEE cells
   const float* inlet_uy;   // nx * nz_global (nullable)
-  const float* outlet_uy;  // nx * nz_global (nullable)
+  const float* outlet_uy;
   int case_kind;
   float lid_u;
-  int nx, ny, pitch, planes;
-  int64_t plane;
-  int z_offset;            // global z of local plane 0
-  int nz_global;           // extent of the boundary tables in z
+  int nx, ny, pitch;
+  int64_t plane, ncell;
+  int z_offset, nz_global;
 };
 hipError_t launch_classify(const GeoArgs& g, hipStream_t s);
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s);
-// LDC cavity codes generated from global coordinates (ldc.cu:468-502)
-hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int planes, int64_t plane,
-                            int z_offset, int nz_global, hipStream_t s);
+hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int64_t plane, int64_t ncell, int z_offset,
+                            int nz_global, hipStream_t s);
 
-// initial populations: form 0 = LDC wi form, 1 = expanded; fields in storage layout
-// (nullable -> rho 1, u 0); writes both buffers over every storage cell
-hipError_t launch_init_feq(float* fa, float* fb, int64_t qstride, int64_t ncell_storage,
-                           int form, const float* rho, const float* ux, const float* uy,
-                           const float* uz, hipStream_t s);
-// LDC initial state from global coordinates (ldc.cu:504-580)
-hipError_t launch_init_ldc(float* fa, float* fb, int64_t qstride, int nx, int ny, int pitch,
-                           int planes, int64_t plane, int z_offset, float lid_u, hipStream_t s);
+// initial populations from per-cell fields (nullable -> rho 1, u 0); form 0 = LDC wi form,
+// 1 = expanded; writes both buffers for every cell
+hipError_t launch_init_feq(float* fa, float* fb, int64_t ncell, int form, const float* rho, const float* ux,
+                           const float* uy, const float* uz, hipStream_t s);
+hipError_t launch_init_ldc(float* fa, float* fb, int64_t ncell, int pitch, int ny, float lid_u, hipStream_t s);
 
 }  // namespace lbm

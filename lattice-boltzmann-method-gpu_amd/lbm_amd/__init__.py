@@ -66,7 +66,8 @@ class lbm_desc(C.Structure):
 LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
-    "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
+    "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells",
+    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
 ]
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
@@ -140,6 +141,8 @@ def lbm_lib() -> C.CDLL:
             "lbm_get_counts": (C.c_int, [P, i64p, i64p, f64p]),
             "lbm_profile": (C.c_int, [P, C.c_int]),
             "lbm_stats": (C.c_int, [P, f64p, i64p, f64p]),
+            "lbm_kernel_times": (C.c_int, [P, C.c_int, f64p, i64p]),
+            "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
@@ -347,7 +350,9 @@ class Lattice:
     def counts(self):
         nb, nf, by = C.c_int64(), C.c_int64(), C.c_double()
         self._ck(lbm_lib().lbm_get_counts(self.h, C.byref(nb), C.byref(nf), C.byref(by)), "lbm_get_counts")
-        return {"n_box": nb.value, "n_fluid": nf.value, "algo_bytes_per_step": by.value}
+        ns = C.c_int64()
+        self._ck(lbm_lib().lbm_get_boundary_cells(self.h, C.byref(ns)), "lbm_get_boundary_cells")
+        return {"n_box": nb.value, "n_fluid": nf.value, "algo_bytes_per_step": by.value, "n_boundary": ns.value}
 
     def profile(self, enabled: bool = True):
         self._ck(lbm_lib().lbm_profile(self.h, 1 if enabled else 0), "lbm_profile")
@@ -355,7 +360,12 @@ class Lattice:
     def stats(self):
         ms, n, by = C.c_double(), C.c_int64(), C.c_double()
         self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
-        return {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
+        out = {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
+        for kind, name in ((0, "stream_collide"), (1, "boundary_fixup")):
+            m, k = C.c_double(), C.c_int64()
+            self._ck(lbm_lib().lbm_kernel_times(self.h, kind, C.byref(m), C.byref(k)), "lbm_kernel_times")
+            out[name + "_ms"], out[name + "_launches"] = m.value, k.value
+        return out
 
     def attach_rccl(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

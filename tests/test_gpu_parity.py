@@ -51,7 +51,7 @@ def test_ldc_bitwise(gpu, oracle, n, steps):
     for s in steps:
         hg = lat.step(s)
         ho = o.step(s)
-        assert_bitwise(lat, o, geo, 0, f"ldc{n} after {o.steps_done if hasattr(o, 'steps_done') else s}")
+        assert_bitwise(lat, o, geo, 0, f"ldc{n} +{s}")
         assert_residuals(hg, ho)
 
 
