@@ -158,7 +158,6 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
   if (r.nchunks > 0) {
     MainArgs a{};
     a.src = src; a.dst = dst; a.type = c->type; a.links = c->links;
-    a.bb_active = (!first || c->bb_immediate) ? 1 : 0;
     a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
     a.partial = r.part;
     a.chunks = r.chunks; a.nchunks = r.nchunks;
@@ -171,12 +170,11 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
   }
   if (r.nslow > 0) {
     FixArgs f{};
-    f.src = src; f.dst = dst; f.type = c->type;
+    f.src = src; f.dst = dst; f.type = c->type; f.links = c->links;
     f.rho = c->rho; f.ux = c->ux; f.uy = c->uy; f.uz = c->uz;
     f.prev = r.prev; f.cells = r.cells; f.n = r.nslow;
     f.pitch = c->L.pitch; f.plane = c->L.plane;
     f.tau = c->tau; f.omc = c->omc;
-    f.bb_active = (!first || c->bb_immediate) ? 1 : 0;
     f.nee_active = first ? 0 : 1;
     f.store_all_macros = store_all ? 1 : 0;
     f.partial = r.part + (r.nchunks > 0 ? main_grid(r.nchunks) : 0);
@@ -243,6 +241,10 @@ int reset_state(lbm_ctx* c) {
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
   for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid})
     if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
+  if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
+    HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+  }
   c->steps_done = 0;
   c->halo_primed = false;
   return LBM_OK;
@@ -532,9 +534,15 @@ int pack_faces(lbm_ctx* c, int b, bool all, hipStream_t st) {
 // unpack what arrived into the ghost planes of buffer b
 int unpack_faces(lbm_ctx* c, int b, bool all, bool from_dn, bool from_up, hipStream_t st) {
   const int nq = all ? kQ : 5;
-  if (from_dn) HIPCK(c, launch_unpack(c->buf[b], c->recv_dn, 0, c->L.plane, all ? qset(c, 2) : qset(c, 0), nq, st));
+  // per step: walls keep their producers' bounce-back values, NEE cells are not pulled;
+  // the initial all-19 copy fills both (raw pulls at step 0) except LDC's primed walls
+  const unsigned skip = (!all || c->bb_immediate ? 1u << kWall : 0u) | (!all ? 1u << kNee : 0u);
+  if (from_dn)
+    HIPCK(c, launch_unpack(c->buf[b], c->recv_dn, c->type, 0, c->L.plane, all ? qset(c, 2) : qset(c, 0), nq, skip,
+                           st));
   if (from_up)
-    HIPCK(c, launch_unpack(c->buf[b], c->recv_up, c->L.nz + 1, c->L.plane, all ? qset(c, 2) : qset(c, 1), nq, st));
+    HIPCK(c, launch_unpack(c->buf[b], c->recv_up, c->type, c->L.nz + 1, c->L.plane, all ? qset(c, 2) : qset(c, 1), nq,
+                           skip, st));
   return LBM_OK;
 }
 

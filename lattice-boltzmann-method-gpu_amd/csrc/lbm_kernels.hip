@@ -7,11 +7,11 @@
 //                    lane: 19 aligned 16-B pulls (x neighbours by a DPP lane shift, the two
 //                    edge lanes read one extra float), moments, equilibria and BGK
 //                    relaxation in registers, 19 16-B stores into the chunk.
-//                    Boundaries are evaluated on the CONSUMER side: a population pulled
-//                    from a wall W at c - e_q is replaced, in the lanes holding wall-
-//                    adjacent cells only, by f_q = src[opp q][c] (half-way bounce-back:
-//                    the value Poiseulle.cu:601-746 / ldc.cu:184-201 put into W one pass
-//                    earlier), selected by a per-cell wall-link bit mask.
+//                    Half-way bounce-back costs no extra pass and no extra round trip:
+//                    a wall-adjacent cell also stores its outgoing population opp(q) into
+//                    the slot q of the wall it pulls q from next step (producer side; the
+//                    value Poiseulle.cu:601-746 / ldc.cu:184-201 write there), so every
+//                    pull is a plain load.
 //  k_boundary_fixup  one thread per fluid cell next to an NEE cell (a compact list of
 //                    contiguous rows, ~0.2% of the cells at 512^3): re-does the cell and
 //                    overwrites it, with
@@ -96,19 +96,36 @@ __device__ __forceinline__ void relax4(f4* v, float tau, float r, float ux, floa
 
 using AllQ = std::make_integer_sequence<int, kQ>;
 
-// half-way bounce-back for cell J of the lane: a population pulled from a wall is replaced by
-// the cell's own opposite population (the value Poiseulle.cu:601-746 / ldc.cu:184-201 store in
-// the wall one pass earlier)
-template <int J, int Q>
-__device__ __forceinline__ void bb_one(f4* v, const float* __restrict__ src, int64_t c, uint32_t m) {
+// Half-way bounce-back, producer side: a wall-adjacent fluid cell F also stores its
+// post-collision population opp(q) into the slot q of the wall W = F - e_q, which F itself
+// pulls at the next step -- exactly the value boundary_stream writes there
+// (Poiseulle.cu:601-746: d_dst[q][W] = d_dst[opp q][W + e_q]).  Each wall slot has one
+// writer (W + e_q), the consumer, so the slot always lives in the writer's own storage.
+template <int Q>
+__device__ __forceinline__ void bb_store_one(float* __restrict__ dst, int64_t c, uint32_t m, float out_opp,
+                                             int pitch, int64_t plane) {
   if constexpr (Q > 0) {
-    if (m & (1u << Q)) v[Q][J] = src[aidx(c + J, Dir<Q>::opp)];
+    if (m & (1u << Q)) dst[aidx(c - (Dir<Q>::x + row_off<Q>(pitch, plane)), Q)] = out_opp;
   }
 }
-template <int J, int... Qs>
-__device__ __forceinline__ void bb_cell(f4* v, const float* __restrict__ src, int64_t c, uint32_t m,
-                                        std::integer_sequence<int, Qs...>) {
-  (bb_one<J, Qs>(v, src, c, m), ...);
+// one set bit at a time (rare path: keeps the address arithmetic out of the hot registers)
+template <int J>
+__device__ __forceinline__ void bb_store_cell(float* __restrict__ dst, int64_t c, uint32_t m, const f4* v, int pitch,
+                                              int64_t plane) {
+#define LBM_BB_CASE(Q) \
+  case Q: dst[aidx(c + J - (Dir<Q>::x + row_off<Q>(pitch, plane)), Q)] = v[Dir<Q>::opp][J]; break;
+  // opaque copy of c: otherwise the compiler CSEs these offsets with the pull addresses of
+  // the same directions and keeps ~70 VGPRs of them alive across the collision (240 vs 167)
+  asm volatile("" : "+v"(c));
+  for (; m; m &= m - 1) {
+    switch (__builtin_ctz(m)) {
+      LBM_BB_CASE(1) LBM_BB_CASE(2) LBM_BB_CASE(3) LBM_BB_CASE(4) LBM_BB_CASE(5) LBM_BB_CASE(6)
+      LBM_BB_CASE(7) LBM_BB_CASE(8) LBM_BB_CASE(9) LBM_BB_CASE(10) LBM_BB_CASE(11) LBM_BB_CASE(12)
+      LBM_BB_CASE(13) LBM_BB_CASE(14) LBM_BB_CASE(15) LBM_BB_CASE(16) LBM_BB_CASE(17) LBM_BB_CASE(18)
+      default: break;
+    }
+  }
+#undef LBM_BB_CASE
 }
 
 // moments (ldc.cu:316-322): sequential fp32 sum; signed sums in the reference order
@@ -137,12 +154,15 @@ __global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
     f4 v[kQ];
     pull4_all(v, a.src, c, lane, a.pitch, a.plane, AllQ{});
     const unsigned t4 = *reinterpret_cast<const unsigned*>(a.type + c);
+    // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
+    // so this dependent load hides behind the arithmetic)
     constexpr unsigned kWall4 = kWallAdj * 0x01010101u;
-    if (a.bb_active && (t4 & kWall4)) {  // rare, divergent: lanes holding wall-adjacent cells
-      if (t4 & (kWallAdj << 0)) bb_cell<0>(v, a.src, c, a.links[c + 0], AllQ{});
-      if (t4 & (kWallAdj << 8)) bb_cell<1>(v, a.src, c, a.links[c + 1], AllQ{});
-      if (t4 & (kWallAdj << 16)) bb_cell<2>(v, a.src, c, a.links[c + 2], AllQ{});
-      if (t4 & (kWallAdj << 24)) bb_cell<3>(v, a.src, c, a.links[c + 3], AllQ{});
+    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    if (t4 & kWall4) {
+      if (t4 & (kWallAdj << 0)) m0 = a.links[c + 0];
+      if (t4 & (kWallAdj << 8)) m1 = a.links[c + 1];
+      if (t4 & (kWallAdj << 16)) m2 = a.links[c + 2];
+      if (t4 & (kWallAdj << 24)) m3 = a.links[c + 3];
     }
     float r0, r1, r2, r3, x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
     collide_cell<0>(v, a.tau, r0, x0, y0, z0);
@@ -160,6 +180,12 @@ __global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
         store |= 1u << j;
         if (!(t & kNeedsMac)) acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
       }
+    }
+    if (t4 & kWall4) {  // rare, divergent: lanes holding wall-adjacent cells
+      if (store & 1u) bb_store_cell<0>(a.dst, c, m0, v, a.pitch, a.plane);
+      if (store & 2u) bb_store_cell<1>(a.dst, c, m1, v, a.pitch, a.plane);
+      if (store & 4u) bb_store_cell<2>(a.dst, c, m2, v, a.pitch, a.plane);
+      if (store & 8u) bb_store_cell<3>(a.dst, c, m3, v, a.pitch, a.plane);
     }
     float* d = a.dst + aidx(c, 0);
     if (store == 0xfu) {
@@ -200,9 +226,7 @@ __device__ __forceinline__ void fix_pull(float* f, const FixArgs& a, int64_t c, 
   if constexpr (Q == 0) return;
   const uint8_t tn = a.type[nb];
   const int cls = tn & kClassMask;
-  if (cls == kWall) {
-    if (a.bb_active) f[Q] = a.src[aidx(c, Dir<Q>::opp)];
-  } else if (cls == kNee) {
+  if (cls == kNee) {
     if (a.nee_active && ((face_bits<Q>() >> nee_face(tn)) & 1)) {
       float rb, bx, by, bz;
       if (tn & kKindPressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
@@ -227,9 +251,15 @@ __device__ __forceinline__ void fix_pull_all(float* f, const FixArgs& a, int64_t
 }
 
 template <int... Qs>
-__device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, float tau, float r,
-                                              float ux, float uy, float uz, std::integer_sequence<int, Qs...>) {
-  ((dst[aidx(c, Qs)] = f[Qs] - (f[Qs] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
+__device__ __forceinline__ void fix_relax_all(float* f, float tau, float r, float ux, float uy, float uz,
+                                              std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = f[Qs] - (f[Qs] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
+}
+template <int... Qs>
+__device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m,
+                                              int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
+  ((dst[aidx(c, Qs)] = f[Qs]), ...);
+  if (m) (bb_store_one<Qs>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
 }
 
 __global__ __launch_bounds__(256) void k_boundary_fixup(const FixArgs a) {
@@ -249,7 +279,8 @@ __global__ __launch_bounds__(256) void k_boundary_fixup(const FixArgs a) {
     const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
     const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
     const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-    fix_store_all(f, a.dst, c, a.tau, rho, ux, uy, uz, AllQ{});
+    fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
+    fix_store_all(f, a.dst, c, a.links[c], a.pitch, a.plane, AllQ{});
     a.prev[i] = make_float4(rho, ux, uy, uz);
     if (a.store_all_macros) {
       a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
@@ -315,13 +346,33 @@ __global__ void k_pack(const float* __restrict__ f, float* __restrict__ buf, int
   }
 }
 
-__global__ void k_unpack(float* __restrict__ f, const float* __restrict__ buf, int zs, int64_t plane,
-                         const int* __restrict__ qs, int nq) {
+// skip_classes (bit per cell class): wall cells keep the bounce-back values their local
+// producers stored (their consumer is on this rank); NEE cells are pulled raw only at step 0
+__global__ void k_unpack(float* __restrict__ f, const float* __restrict__ buf, const uint8_t* __restrict__ type,
+                         int zs, int64_t plane, const int* __restrict__ qs, int nq, unsigned skip_classes) {
   const int64_t n = plane * nq;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int k = (int)(i / plane);
     const int64_t c = (int64_t)zs * plane + (i - k * plane);
+    const int cls = type[c] & kClassMask;
+    if ((skip_classes >> cls) & 1u) continue;
     f[aidx(c, qs[k])] = buf[i];
+  }
+}
+
+// LDC bounce-back already at step 0 (ldc.cu:75-202 swaps in place before the fluid reads):
+// seed the wall slots of buffer f from the initial populations, as the producers would have
+template <int... Qs>
+__device__ __forceinline__ void prime_cell(float* f, int64_t c, uint32_t m, int pitch, int64_t plane,
+                                           std::integer_sequence<int, Qs...>) {
+  (bb_store_one<Qs>(f, c, m, f[aidx(c, Dir<Qs>::opp)], pitch, plane), ...);
+}
+__global__ void k_bb_prime(float* f, const uint8_t* __restrict__ type, const uint32_t* __restrict__ links,
+                           int64_t ncell, int pitch, int64_t plane) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t t = type[c];
+    if ((t & kClassMask) != kFluid || !(t & kWallAdj)) continue;
+    prime_cell(f, c, links[c], pitch, plane, AllQ{});
   }
 }
 
@@ -484,8 +535,15 @@ hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const 
   return hipGetLastError();
 }
 
-hipError_t launch_unpack(float* f, const float* buf, int zs, int64_t plane, const int* qs, int nq, hipStream_t s) {
-  hipLaunchKernelGGL(k_unpack, dim3(grid_for(plane * nq, 256)), dim3(256), 0, s, f, buf, zs, plane, qs, nq);
+hipError_t launch_unpack(float* f, const float* buf, const uint8_t* type, int zs, int64_t plane, const int* qs, int nq,
+                         unsigned skip_classes, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack, dim3(grid_for(plane * nq, 256)), dim3(256), 0, s, f, buf, type, zs, plane, qs, nq, skip_classes);
+  return hipGetLastError();
+}
+
+hipError_t launch_bb_prime(float* f, const uint8_t* type, const uint32_t* links, int64_t ncell, int pitch, int64_t plane,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_bb_prime, dim3(grid_for(ncell, 256)), dim3(256), 0, s, f, type, links, ncell, pitch, plane);
   return hipGetLastError();
 }
 

@@ -41,6 +41,7 @@ struct MainArgs {
   float* dst;
   const uint8_t* type;  // per cell
   const uint32_t* links;  // per cell: bit q set when c - e_q is a wall (read for kWallAdj cells)
+                          // -> producer-side bounce-back stores
   float* rho; float* ux; float* uy; float* uz;
   double* partial;      // one per block
   const int* chunks;    // active chunk ids
@@ -49,7 +50,6 @@ struct MainArgs {
   int64_t plane;
   int64_t c_lo, c_hi;   // cell range of this launch (cells outside are not touched)
   float tau;
-  int bb_active;        // wall neighbours bounce back (else raw pull: reference step 0)
   int store_all_macros;
   const int* stopped;   // nullable
 };
@@ -60,6 +60,7 @@ struct FixArgs {
   const float* src;
   float* dst;
   const uint8_t* type;
+  const uint32_t* links;
   float* rho; float* ux; float* uy; float* uz;  // full fields; NEE data sits at NEE cells
   float4* prev;         // per slow cell: its (rho, ux, uy, uz) of the previous step
   const int* cells;     // slow cell ids (linear)
@@ -67,7 +68,7 @@ struct FixArgs {
   int pitch;
   int64_t plane;
   float tau, omc;
-  int bb_active, nee_active, store_all_macros;
+  int nee_active, store_all_macros;
   double* partial;
   const int* stopped;
 };
@@ -101,8 +102,12 @@ hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s
 // halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack
 hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const int* qs_dev, int nq,
                        hipStream_t s);
-hipError_t launch_unpack(float* f, const float* buf, int zs, int64_t plane, const int* qs_dev, int nq,
-                         hipStream_t s);
+// skip_classes: bit (1 << class) leaves ghost cells of that class untouched
+hipError_t launch_unpack(float* f, const float* buf, const uint8_t* type, int zs, int64_t plane, const int* qs_dev,
+                         int nq, unsigned skip_classes, hipStream_t s);
+// seed wall slots with bounce-back values of buffer f (LDC: bounce-back already at step 0)
+hipError_t launch_bb_prime(float* f, const uint8_t* type, const uint32_t* links, int64_t ncell, int pitch,
+                           int64_t plane, hipStream_t s);
 
 // geometry: reference codes (int8 per linear cell) -> cell-type bytes
 struct GeoArgs {
