@@ -64,28 +64,41 @@ constexpr int64_t row_off(int pitch, int64_t plane) {
   return Dir<Q>::y * (int64_t)pitch + Dir<Q>::z * plane;
 }
 
-// population Q of the lane's 4 cells c..c+3, pulled from c - e_Q .. c+3 - e_Q
+// Pull of population Q for the lane's 4 cells c..c+3 from c - e_Q .. c+3 - e_Q, in two
+// phases so that all of a wave's loads are in flight together (one round trip per wave):
+//  issue:   the aligned 16-B slice at c - (e_Q with e_x = 0), and for e_x != 0 the one
+//           float the wave's edge lane needs from the neighbouring chunk -- a wave-uniform
+//           address (chunk base cb), so a scalar load with no branch;
+//  compose: shift the slice by one cell across lanes (DPP) and drop the edge float into
+//           lane 0 (e_x = +1) or lane 63 (e_x = -1).
 template <int Q>
-__device__ __forceinline__ f4 pull4(const float* __restrict__ src, int64_t c, int lane, int pitch, int64_t plane) {
-  const int64_t b = c - row_off<Q>(pitch, plane);
-  const f4 a = *reinterpret_cast<const f4*>(src + aidx(b, Q));
+__device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t cb, int64_t c,
+                                           int pitch, int64_t plane) {
+  const int64_t ro = row_off<Q>(pitch, plane);
+  a = *reinterpret_cast<const f4*>(src + aidx(c - ro, Q));
+  if constexpr (Dir<Q>::x == 1) e = src[aidx(cb - ro - 1, Q)];                  // lane 0: b - 1
+  else if constexpr (Dir<Q>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];       // lane 63: b + 4
+}
+
+template <int Q>
+__device__ __forceinline__ f4 pull_compose(const f4 a, float e, int lane) {
   if constexpr (Dir<Q>::x == 0) {
     return a;
   } else if constexpr (Dir<Q>::x == 1) {  // needs b-1 .. b+2
-    float p = lane_from_prev(a.w);
-    if (lane == 0) p = src[aidx(b - 1, Q)];
-    return f4{p, a.x, a.y, a.z};
+    const float p = lane_from_prev(a.w);
+    return f4{lane == 0 ? e : p, a.x, a.y, a.z};
   } else {                                 // needs b+1 .. b+4
-    float n = lane_from_next(a.x);
-    if (lane == 63) n = src[aidx(b + 4, Q)];
-    return f4{a.y, a.z, a.w, n};
+    const float n = lane_from_next(a.x);
+    return f4{a.y, a.z, a.w, lane == 63 ? e : n};
   }
 }
 
 template <int... Qs>
-__device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t c, int lane, int pitch,
-                                          int64_t plane, std::integer_sequence<int, Qs...>) {
-  ((v[Qs] = pull4<Qs>(src, c, lane, pitch, plane)), ...);
+__device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t cb, int64_t c, int lane,
+                                          int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
+  float e[kQ];
+  ((pull_issue<Qs>(v[Qs], e[Qs], src, cb, c, pitch, plane)), ...);
+  ((v[Qs] = pull_compose<Qs>(v[Qs], e[Qs], lane)), ...);
 }
 
 template <int J, int... Qs>
@@ -149,10 +162,10 @@ __global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
   const int idx = blockIdx.x * (kBlock / 64) + wave;
   double acc = 0.0;
   if (idx < a.nchunks) {
-    const int64_t ch = a.chunks[idx];
-    const int64_t c = ch * kChunk + lane * 4;
+    const int64_t cb = (int64_t)a.chunks[idx] * kChunk;  // wave-uniform chunk base
+    const int64_t c = cb + lane * 4;
     f4 v[kQ];
-    pull4_all(v, a.src, c, lane, a.pitch, a.plane, AllQ{});
+    pull4_all(v, a.src, cb, c, lane, a.pitch, a.plane, AllQ{});
     const unsigned t4 = *reinterpret_cast<const unsigned*>(a.type + c);
     // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
     // so this dependent load hides behind the arithmetic)

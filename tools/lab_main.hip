@@ -1,0 +1,227 @@
+// lab_main.hip -- ablation bench of the production stream-collide kernel (tools only).
+//
+// Includes the product kernel source so every helper (pull4, collide_cell, bb_store_cell,
+// block_sum) is the shipped one, and times copies of k_stream_collide with features
+// switched off one at a time on a 512^3 LDC-like box (fluid 2..509, walls at 1 and 510).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
+//     -fhip-fp32-correctly-rounded-divide-sqrt -o tools/lab_main tools/lab_main.hip
+#include "../lattice-boltzmann-method-gpu_amd/csrc/lbm_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) {                                                                    \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(1);                                                                            \
+    }                                                                                          \
+  } while (0)
+
+using namespace lbm;
+
+enum : int { F_LIST = 1, F_STOP = 2, F_BSUM = 4, F_UABS = 8, F_BB = 16, F_MASK = 32, F_ALL = 63 };
+
+template <int F, int MINW = 1, int WPB = 4>
+__global__ __launch_bounds__(WPB * 64, MINW) void k_var(const MainArgs a, int ch0) {
+  __shared__ double red[WPB];
+  if constexpr (F & F_STOP)
+    if (a.stopped != nullptr && *a.stopped) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int idx = blockIdx.x * WPB + wave;
+  double acc = 0.0;
+  if (idx < a.nchunks) {
+    const int64_t cb = (int64_t)((F & F_LIST) ? a.chunks[idx] : ch0 + idx) * kChunk;
+    const int64_t c = cb + lane * 4;
+    f4 v[kQ];
+    pull4_all(v, a.src, cb, c, lane, a.pitch, a.plane, AllQ{});
+    const unsigned t4 = *reinterpret_cast<const unsigned*>(a.type + c);
+    constexpr unsigned kWall4 = kWallAdj * 0x01010101u;
+    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    if constexpr (F & F_BB) {
+      if (t4 & kWall4) {
+        if (t4 & (kWallAdj << 0)) m0 = a.links[c + 0];
+        if (t4 & (kWallAdj << 8)) m1 = a.links[c + 1];
+        if (t4 & (kWallAdj << 16)) m2 = a.links[c + 2];
+        if (t4 & (kWallAdj << 24)) m3 = a.links[c + 3];
+      }
+    }
+    float r0, r1, r2, r3, x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
+    collide_cell<0>(v, a.tau, r0, x0, y0, z0);
+    collide_cell<1>(v, a.tau, r1, x1, y1, z1);
+    collide_cell<2>(v, a.tau, r2, x2, y2, z2);
+    collide_cell<3>(v, a.tau, r3, x3, y3, z3);
+    const f4 R{r0, r1, r2, r3}, UX{x0, x1, x2, x3}, UY{y0, y1, y2, y3}, UZ{z0, z1, z2, z3};
+    unsigned store = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned t = (t4 >> (8 * j)) & 0xffu;
+      const int64_t cj = c + j;
+      bool in;
+      if constexpr (F & F_MASK) in = cj >= a.c_lo && cj < a.c_hi && (t & kClassMask) == kFluid;
+      else in = (t & kClassMask) == kFluid;
+      if (in) {
+        store |= 1u << j;
+        if constexpr (F & F_UABS)
+          if (!(t & kNeedsMac)) acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
+      }
+    }
+    if constexpr (F & F_BB) {
+      if (t4 & kWall4) {
+        if (store & 1u) bb_store_cell<0>(a.dst, c, m0, v, a.pitch, a.plane);
+        if (store & 2u) bb_store_cell<1>(a.dst, c, m1, v, a.pitch, a.plane);
+        if (store & 4u) bb_store_cell<2>(a.dst, c, m2, v, a.pitch, a.plane);
+        if (store & 8u) bb_store_cell<3>(a.dst, c, m3, v, a.pitch, a.plane);
+      }
+    }
+    float* d = a.dst + aidx(c, 0);
+    if (store == 0xfu) {
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));
+      if (a.store_all_macros) {
+        *reinterpret_cast<f4*>(a.rho + c) = R;
+        *reinterpret_cast<f4*>(a.ux + c) = UX;
+        *reinterpret_cast<f4*>(a.uy + c) = UY;
+        *reinterpret_cast<f4*>(a.uz + c) = UZ;
+      }
+    } else if (store) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!(store & (1u << j))) continue;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) d[q * kChunk + j] = v[q][j];
+      }
+    }
+  }
+  if constexpr (F & F_BSUM) {
+    const double s = block_sum(acc, red);
+    if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
+  } else {
+    if (acc == -1.0) a.partial[blockIdx.x] = acc;
+  }
+}
+
+__global__ void k_lab_type(uint8_t* type, uint32_t* links, int n, int pitch, int64_t plane, int64_t ncell) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(c % pitch), y = (int)((c / pitch) % n), z = (int)(c / plane) - 1;
+    auto cls = [&](int xx, int yy, int zz) -> uint8_t {
+      if (xx < 1 || yy < 1 || zz < 1 || xx > n - 2 || yy > n - 2 || zz > n - 2) return kPassive;
+      if (xx == 1 || yy == 1 || zz == 1 || xx == n - 2 || yy == n - 2 || zz == n - 2) return kWall;
+      return kFluid;
+    };
+    uint8_t t = cls(x, y, z);
+    uint32_t m = 0;
+    if (t == kFluid) {
+      for (int q = 1; q < kQ; ++q)
+        if (cls(x - kEx[q], y - kEy[q], z - kEz[q]) == kWall) m |= 1u << q;
+      if (m) t |= kWallAdj;
+    }
+    type[c] = t;
+    links[c] = m;
+  }
+}
+
+__global__ void k_lab_fill(float* a, int64_t n, float amp) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    a[i] = 1.0f / 19.0f + amp * (float)(i % 7);
+}
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? std::atoi(argv[1]) : 512;
+  const int rounds = argc > 2 ? std::atoi(argv[2]) : 5;
+  const float amp = argc > 3 ? (float)std::atof(argv[3]) : 1e-4f;  // 0: uniform rest state
+  Layout L{};
+  L.nx = L.ny = L.nz = N;
+  L.pitch = N;
+  L.planes = N + 2;
+  L.plane = (int64_t)N * N;
+  L.ncell = (L.plane * L.planes + kChunk - 1) / kChunk * kChunk;
+  L.nchunk = L.ncell / kChunk;
+  L.guard = (L.plane + L.pitch + 1 + kChunk - 1) / kChunk + 1;
+  float *A, *B, *mac;
+  uint8_t* type;
+  uint32_t* links;
+  int *chunks, *stopped;
+  double* part;
+  CK(hipMalloc(&A, sizeof(float) * L.buf_floats()));
+  CK(hipMalloc(&B, sizeof(float) * L.buf_floats()));
+  CK(hipMalloc(&mac, sizeof(float) * L.ncell * 4));
+  CK(hipMalloc(&type, L.ncell + 64));
+  CK(hipMalloc(&links, sizeof(uint32_t) * (L.ncell + 64)));
+  CK(hipMalloc(&stopped, sizeof(int)));
+  CK(hipMemset(stopped, 0, sizeof(int)));
+  hipLaunchKernelGGL(k_lab_fill, dim3(8192), dim3(256), 0, 0, A, L.buf_floats(), amp);
+  hipLaunchKernelGGL(k_lab_fill, dim3(8192), dim3(256), 0, 0, B, L.buf_floats(), amp);
+  hipLaunchKernelGGL(k_lab_type, dim3(8192), dim3(256), 0, 0, type, links, N, L.pitch, L.plane, L.ncell);
+  // active chunks: storage planes 3 .. N (fluid z 2 .. N-3)
+  const int64_t c_lo = 3 * L.plane, c_hi = (int64_t)(N - 1) * L.plane;
+  const int ch0 = (int)(c_lo / kChunk), nch = (int)((c_hi - c_lo) / kChunk);
+  std::vector<int> hch(nch);
+  for (int i = 0; i < nch; ++i) hch[i] = ch0 + i;
+  CK(hipMalloc(&chunks, sizeof(int) * nch));
+  CK(hipMemcpy(chunks, hch.data(), sizeof(int) * nch, hipMemcpyHostToDevice));
+  CK(hipMalloc(&part, sizeof(double) * (nch + 64)));  // one per block at WPB = 1
+  float* a_base = A + L.guard * kQ * kChunk;
+  float* b_base = B + L.guard * kQ * kChunk;
+  CK(hipDeviceSynchronize());
+  const double fluid = (double)(N - 4) * (N - 4) * (N - 4);
+
+  struct V {
+    const char* name;
+    void (*launch)(const MainArgs&, int, int);
+  };
+#define VAR(NAME, F, MINW, WPB)                                                                                  \
+  V{NAME, [](const MainArgs& m, int c0, int n) {                                                               \
+      hipLaunchKernelGGL((k_var<F, MINW, WPB>), dim3((n + WPB - 1) / WPB), dim3(WPB * 64), 0, 0, m, c0); }}
+  std::vector<V> vs = {
+      VAR("full (production)", F_ALL, 1, 4),
+      VAR("- chunk list", F_ALL & ~F_LIST, 1, 4),
+      VAR("- stopped flag", F_ALL & ~F_STOP, 1, 4),
+      VAR("- block sum", F_ALL & ~F_BSUM, 1, 4),
+      VAR("- |u| accumulate", F_ALL & ~F_UABS, 1, 4),
+      VAR("- bounce-back", F_ALL & ~F_BB, 1, 4),
+      VAR("- range mask", F_ALL & ~F_MASK, 1, 4),
+      VAR("bare (none)", 0, 1, 4),
+      VAR("- list - stop", F_ALL & ~(F_LIST | F_STOP), 1, 4),
+      VAR("full wpb1", F_ALL, 1, 1),
+      VAR("full wpb2", F_ALL, 1, 2),
+      VAR("full lb4", F_ALL, 4, 4),
+      VAR("bare lb4", 0, 4, 4),
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> ms(vs.size());
+  for (int r = 0; r < rounds; ++r) {
+    for (size_t i = 0; i < vs.size(); ++i) {
+      MainArgs m{};
+      m.type = type; m.links = links;
+      m.rho = mac; m.ux = mac + L.ncell; m.uy = mac + 2 * L.ncell; m.uz = mac + 3 * L.ncell;
+      m.partial = part; m.chunks = chunks; m.nchunks = nch; m.pitch = L.pitch; m.plane = L.plane;
+      m.c_lo = c_lo; m.c_hi = c_hi; m.tau = 0.55f; m.store_all_macros = 0; m.stopped = stopped;
+      CK(hipEventRecord(e0));
+      for (int it = 0; it < 4; ++it) {
+        m.src = (it & 1) ? b_base : a_base;
+        m.dst = (it & 1) ? a_base : b_base;
+        vs[i].launch(m, ch0, nch);
+      }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipGetLastError());
+      float t = 0;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ms[i].push_back(t / 4);
+    }
+  }
+  for (size_t i = 0; i < vs.size(); ++i) {
+    std::sort(ms[i].begin(), ms[i].end());
+    const float med = ms[i][ms[i].size() / 2];
+    std::printf("%-22s median %7.3f ms  %8.1f MLUPS(fluid)  %7.1f GB/s (152 B/fluid cell)\n", vs[i].name, med,
+                fluid / (med * 1e-3) / 1e6, 152.0 * fluid / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}
