@@ -76,6 +76,10 @@ typedef struct {
   int device;              /* HIP device ordinal */
   int z_offset;            /* global z of local plane 0 */
   int nz_global;           /* global z extent (== nz for a single-domain run) */
+  /* Row alignment of the device layout: 1..4 = store cell x at x + (x_align - 1); 0 = choose
+   * it from geo so that most rows start their fluid run on a 4-cell boundary.  Slabs of one
+   * lattice must use the same value (lbm_attach_rccl / lbm_group_step check it). */
+  int x_align;
 } lbm_desc;
 
 /* Status / version */

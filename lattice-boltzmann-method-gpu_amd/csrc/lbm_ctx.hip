@@ -109,7 +109,26 @@ struct lbm_ctx {
 namespace {
 
 int64_t cell_of(const Layout& L, int x, int y, int z) {  // local z (storage plane z+1)
-  return (int64_t)x + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
+  return (int64_t)(x + L.xoff) + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
+}
+
+// x offset that puts the most common first-fluid x of a row at a multiple of 4
+int choose_xoff(const lbm_desc& d) {
+  if (d.x_align > 0) return d.x_align - 1;
+  if (!d.geo) return 2;  // device-generated cavity: fluid starts at x = 2 (ldc.cu:469)
+  const int8_t fluid = d.case_kind == LBM_CASE_LDC ? 3 : 4;
+  const int rows = (d.nz + (d.halo_planes ? 2 : 0)) * d.ny;
+  int64_t hist[4] = {0, 0, 0, 0};
+  for (int r = 0; r < rows; ++r) {
+    const int8_t* row = d.geo + (int64_t)r * d.nx;
+    for (int x = 0; x < d.nx; ++x)
+      if (row[x] == fluid) {
+        hist[x & 3]++;
+        break;
+      }
+  }
+  const int best = (int)(std::max_element(hist, hist + 4) - hist);
+  return (4 - best) & 3;
 }
 
 // time one kernel launch with HIP events on its own stream (lbm_profile)
@@ -265,7 +284,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   }
   *out = nullptr;
   const lbm_desc& d = *desc;
-  if (d.nx < 3 || d.ny < 3 || d.nz < 1 || !(d.tau > 0.f) || d.case_kind < 0 || d.case_kind > 2) {
+  if (d.nx < 3 || d.ny < 3 || d.nz < 1 || !(d.tau > 0.f) || d.case_kind < 0 || d.case_kind > 2 || d.x_align < 0 ||
+      d.x_align > 4) {
     g_create_error = "invalid lattice description";
     return LBM_ERR_ARG;
   }
@@ -284,7 +304,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
-  L.pitch = (d.nx + 3) / 4 * 4;
+  L.xoff = choose_xoff(d);
+  L.pitch = (d.nx + L.xoff + 3) / 4 * 4;
   L.planes = d.nz + 2;
   L.plane = (int64_t)L.pitch * L.ny;
   L.ncell = (L.plane * L.planes + kChunk - 1) / kChunk * kChunk;
@@ -356,7 +377,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     CK(hipMemcpyAsync(dcodes, h.data(), L.ncell, hipMemcpyHostToDevice, c->s_comp));
     CK(hipStreamSynchronize(c->s_comp));
   } else {
-    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.plane, L.ncell, d.z_offset, c->d.nz_global, c->s_comp));
+    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.xoff, L.plane, L.ncell, d.z_offset, c->d.nz_global,
+                        c->s_comp));
   }
   const int64_t ntab = (int64_t)d.nx * c->d.nz_global;
   if (desc->bc_inlet_uy) {
@@ -372,7 +394,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   g.rho = c->rho; g.ux = c->ux; g.uy = c->uy; g.uz = c->uz;
   g.inlet_uy = din; g.outlet_uy = dout;
   g.case_kind = d.case_kind; g.lid_u = d.lid_u;
-  g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.plane = L.plane; g.ncell = L.ncell;
+  g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.xoff = L.xoff; g.plane = L.plane; g.ncell = L.ncell;
   g.z_offset = d.z_offset; g.nz_global = c->d.nz_global;
   CK(launch_classify(g, c->s_comp));
   CK(launch_flag_fluid(g, c->s_comp));
@@ -760,6 +782,20 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
   NCCK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
   c->nranks = nranks;
+  {  // every slab must use the same row layout: the halo planes are copied cell for cell
+    int h[2] = {c->L.pitch * 4 + c->L.xoff, -(c->L.pitch * 4 + c->L.xoff)};
+    int* dv = nullptr;
+    HIPCK(c, hipMalloc(&dv, sizeof(h)));
+    HIPCK(c, hipMemcpy(dv, h, sizeof(h), hipMemcpyHostToDevice));
+    NCCK(c, ncclAllReduce(dv, dv, 2, ncclInt, ncclMax, c->comm, c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+    HIPCK(c, hipMemcpy(h, dv, sizeof(h), hipMemcpyDeviceToHost));
+    HIPCK(c, hipFree(dv));
+    if (h[0] != -h[1]) {
+      c->err = "slabs differ in row layout (pitch / x alignment); give every rank the same nx and fluid x range";
+      return LBM_ERR_GEOMETRY;
+    }
+  }
   c->halo_primed = false;
   return LBM_OK;
 }
@@ -793,9 +829,12 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   if (!cs || n < 1 || nsteps < 0) return LBM_ERR_ARG;
   lbm_ctx* c0 = cs[0];
   for (int i = 0; i < n; ++i) {
-    if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.ny != c0->L.ny ||
-        cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled || cs[i]->comm)
+    if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xoff != c0->L.xoff || cs[i]->L.ny != c0->L.ny ||
+        cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled || cs[i]->comm) {
+      c0->err = "lbm_group_step: slabs must share device, row layout (nx, ny, x_align) and step count, "
+                "without convergence control or RCCL";
       return LBM_ERR_ARG;
+    }
   }
   HIPCK(c0, hipSetDevice(c0->d.device));
   hipStream_t st = c0->s_comp;  // one stream: slabs run back to back (test / debug path)

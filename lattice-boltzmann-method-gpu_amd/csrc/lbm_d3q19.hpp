@@ -65,12 +65,13 @@ constexpr int face_bits() {
 // (the cell is re-done by the boundary fix-up kernel, which keeps its previous (rho, u));
 // NEE boundary cell: bits 4-6 face, bit 7 kind (0 velocity, 1 pressure).
 enum : uint8_t {
-  kPassive = 0,   // ghost / unused / padding: never updated, pulled raw (constant)
+  kPassive = 0,   // ghost / unused / padding: never updated; pulled raw (constant) if kPulled
   kWall = 1,      // half-way bounce-back
   kNee = 2,       // non-equilibrium extrapolation boundary cell
   kFluid = 3,     // collide + stream
   kClassMask = 3,
   kWallAdj = 1u << 2,   // fluid with a wall neighbour
+  kPulled = 1u << 2,    // passive cell a fluid cell pulls from (kept constant)
   kNeedsMac = 1u << 3,  // fluid with an NEE neighbour
   kKindPressure = 1u << 7,
 };

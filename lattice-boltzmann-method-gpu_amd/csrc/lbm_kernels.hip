@@ -201,7 +201,15 @@ __global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
       if (store & 8u) bb_store_cell<3>(a.dst, c, m3, v, a.pitch, a.plane);
     }
     float* d = a.dst + aidx(c, 0);
-    if (store == 0xfu) {
+    // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
+    // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
+    // bounce-back slots / boundary data and cells outside [c_lo, c_hi) belong to another
+    // launch, so those lanes store cell by cell -- sub-16-B stores cost whole partial-line
+    // writes in HBM (the x-ends of every row took 15% of the step before xoff alignment).
+    const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
+    const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
+    const bool keep_others = special != 0u || c < a.c_lo || c + 4 > a.c_hi;
+    if (store == 0xfu || (store != 0u && !keep_others)) {
 #pragma unroll
       for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));
       if (a.store_all_macros) {
@@ -396,11 +404,11 @@ __global__ void k_classify(const GeoArgs g) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int code = g.codes[c];
-    const int x = (int)(c % g.pitch);
+    const int x = (int)(c % g.pitch) - g.xoff;
     const int zs = (int)(c / g.plane);
     const int zg = zs - 1 + g.z_offset;  // global z
     uint8_t t = kPassive;
-    if (x < g.nx) {
+    if (x >= 0 && x < g.nx) {
       if (g.case_kind == 0) {  // LDC (ldc.cu:469): 0 ghost, 1 wall, 2 lid, 3 fluid
         if (code == 1) t = kWall;
         else if (code == 3) t = kFluid;
@@ -465,15 +473,32 @@ __global__ void k_flag_fluid(const GeoArgs g) {
   }
 }
 
-__global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int64_t plane, int64_t ncell, int z_offset,
-                            int nzg) {
+// passive cells some fluid cell pulls from (malformed geometry, the reference reads their
+// initial values forever): flag them so the main kernel never overwrites them
+template <int... Qs>
+__device__ __forceinline__ bool pulled_by_fluid(const uint8_t* type, int64_t c, const GeoArgs& g,
+                                                std::integer_sequence<int, Qs...>) {
+  auto fl = [&](int64_t n) { return n >= 0 && n < g.ncell && (type[n] & kClassMask) == kFluid; };
+  return (fl(c + Dir<Qs>::x + Dir<Qs>::y * (int64_t)g.pitch + Dir<Qs>::z * g.plane) || ...);
+}
+
+__global__ void k_mark_pulled(const GeoArgs g) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t t = g.type[c];
+    if ((t & kClassMask) == kPassive && pulled_by_fluid(g.type, c, g, AllQ{})) g.type[c] = (uint8_t)(t | kPulled);
+  }
+}
+
+__global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xoff, int64_t plane, int64_t ncell,
+                            int z_offset, int nzg) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const int x = (int)(c % pitch);
+    const int x = (int)(c % pitch) - xoff;
     const int y = (int)((c / pitch) % ny);
     const int z = (int)(c / plane) - 1 + z_offset;
     int8_t code = 0;  // ldc.cu:468-502
-    if (x < nx && z >= 0 && z < nzg) {
+    if (x >= 0 && x < nx && z >= 0 && z < nzg) {
       if (x >= 1 && x < nx - 1 && y >= 1 && y < ny - 1 && z >= 1 && z < nzg - 1) code = 1;
       if (x >= 2 && x < nx - 2 && y >= 2 && y < ny - 2 && z >= 2 && z < nzg - 2) code = 3;
       if (y == ny - 2 && x >= 1 && x < nx - 1 && z >= 1 && z < nzg - 1) code = 2;
@@ -567,13 +592,14 @@ hipError_t launch_classify(const GeoArgs& g, hipStream_t s) {
 
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s) {
   hipLaunchKernelGGL(k_flag_fluid, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_mark_pulled, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
-hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int64_t plane, int64_t ncell, int z_offset,
-                            int nz_global, hipStream_t s) {
-  hipLaunchKernelGGL(k_ldc_codes, dim3(grid_for(ncell, 256)), dim3(256), 0, s, codes, nx, ny, pitch, plane, ncell,
-                     z_offset, nz_global);
+hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xoff, int64_t plane, int64_t ncell,
+                            int z_offset, int nz_global, hipStream_t s) {
+  hipLaunchKernelGGL(k_ldc_codes, dim3(grid_for(ncell, 256)), dim3(256), 0, s, codes, nx, ny, pitch, xoff, plane,
+                     ncell, z_offset, nz_global);
   return hipGetLastError();
 }
 

@@ -23,7 +23,10 @@ __host__ __device__ __forceinline__ int64_t aidx(int64_t c, int q) {
 
 struct Layout {
   int nx, ny, nz;
-  int pitch;          // multiple of 4
+  int xoff;           // storage x = x + xoff: puts the first fluid cell of a row at a
+                      // multiple of 4, so fluid 4-cell lane groups hold no wall cells
+                      // (those groups store whole 16-B vectors; see k_stream_collide)
+  int pitch;          // >= nx + xoff, multiple of 4
   int planes;         // nz + 2
   int64_t plane;      // pitch * ny
   int64_t ncell;      // plane * planes rounded up to a whole chunk
@@ -119,13 +122,13 @@ struct GeoArgs {
   const float* outlet_uy;
   int case_kind;
   float lid_u;
-  int nx, ny, pitch;
+  int nx, ny, pitch, xoff;
   int64_t plane, ncell;
   int z_offset, nz_global;
 };
 hipError_t launch_classify(const GeoArgs& g, hipStream_t s);
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s);
-hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int64_t plane, int64_t ncell, int z_offset,
+hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xoff, int64_t plane, int64_t ncell, int z_offset,
                             int nz_global, hipStream_t s);
 
 // initial populations from per-cell fields (nullable -> rho 1, u 0); form 0 = LDC wi form,

@@ -59,6 +59,7 @@ class lbm_desc(C.Structure):
         ("device", C.c_int),
         ("z_offset", C.c_int),
         ("nz_global", C.c_int),
+        ("x_align", C.c_int),
     ]
 
 
@@ -216,6 +217,17 @@ def poiseuille_profile(nx: int, nz: int, u_max: float = POIS_UMAX_KERNEL) -> np.
     return t
 
 
+def x_align_for(geo: np.ndarray, case_kind: int) -> int:
+    """lbm_desc.x_align the library would choose for this whole-lattice mask (give the same
+    value to every slab of it): the most common first-fluid x of a row onto a 4-cell boundary."""
+    fluid = 3 if case_kind == LBM_CASE_LDC else 4
+    g = np.ascontiguousarray(geo, np.int8).reshape(-1, geo.shape[-1]) == fluid
+    has = g.any(axis=1)
+    first = np.argmax(g, axis=1)[has]
+    hist = np.bincount(first & 3, minlength=4)
+    return ((4 - int(np.argmax(hist))) & 3) + 1
+
+
 def initial_fields(case_kind: int, geo: np.ndarray, inlet_uy=None, outlet_uy=None):
     g = np.ascontiguousarray(geo, np.int8)
     nz, ny, nx = g.shape
@@ -253,7 +265,7 @@ class Lattice:
 
     def __init__(self, case_kind: int, shape, tau: float, geo: np.ndarray | None = None, *,
                  halo_planes: bool = False, lid_u_val: float | None = None, inlet_uy=None, outlet_uy=None,
-                 device: int = 0, z_offset: int = 0, nz_global: int | None = None):
+                 device: int = 0, z_offset: int = 0, nz_global: int | None = None, x_align: int = 0):
         nz, ny, nx = shape
         self.shape = (nz, ny, nx)
         self.case_kind = case_kind
@@ -279,6 +291,7 @@ class Lattice:
         d.device = device
         d.z_offset = z_offset
         d.nz_global = nz if nz_global is None else nz_global
+        d.x_align = x_align
         self.desc = d
         h = P()
         rc = lbm_lib().lbm_create(C.byref(d), C.byref(h))

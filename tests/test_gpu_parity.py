@@ -162,11 +162,12 @@ def test_loopback_slabs_bitwise(gpu, nslabs):
     one, geo = cases.poiseuille(nx, ny, nz)
     prof = lbm_amd.poiseuille_profile(nx, nz)
     rho, ux, uy, uz = initial_fields(1, geo)
+    xa = lbm_amd.x_align_for(geo, LBM_CASE_POISEUILLE)
     slabs = []
     for i in range(nslabs):
         z0, z1 = cases.slab_bounds(nz, nslabs, i)
         lat = Lattice(LBM_CASE_POISEUILLE, (z1 - z0, ny, nx), 0.58, cases.slab_geo(geo, z0, z1), halo_planes=True,
-                      inlet_uy=prof, outlet_uy=prof, z_offset=z0, nz_global=nz)
+                      inlet_uy=prof, outlet_uy=prof, z_offset=z0, nz_global=nz, x_align=xa)
         lat.init_equilibrium(LBM_INIT_EXPANDED, rho[z0:z1], ux[z0:z1], uy[z0:z1], uz[z0:z1])
         slabs.append((z0, z1, lat))
     h1 = one.step(45)

@@ -23,7 +23,31 @@
 
 using namespace lbm;
 
-enum : int { F_LIST = 1, F_STOP = 2, F_BSUM = 4, F_UABS = 8, F_BB = 16, F_MASK = 32, F_ALL = 63 };
+enum : int { F_LIST = 1, F_STOP = 2, F_BSUM = 4, F_UABS = 8, F_BB = 16, F_MASK = 32, F_ALL = 63, F_FASTDIV = 64, F_FULLSTORE = 128 };
+
+// x / tau as RN(x * RN(1/tau)) refined by one FMA residual step (Markstein)
+template <int J, int... Qs>
+__device__ __forceinline__ void relax4_fast(f4* v, float tau, float y, float r, float ux, float uy, float uz,
+                                            std::integer_sequence<int, Qs...>) {
+  auto dv = [&](float x) {
+    const float q0 = x * y;
+    const float rr = __builtin_fmaf(-q0, tau, x);
+    return __builtin_fmaf(rr, y, q0);
+  };
+  ((v[Qs][J] = v[Qs][J] - dv(v[Qs][J] - feq<Qs>(r, ux, uy, uz))), ...);
+}
+template <int J>
+__device__ __forceinline__ void collide_cell_fast(f4* v, float tau, float y, float& rho, float& ux, float& uy,
+                                                  float& uz) {
+  float r = 0.f;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) r = r + v[q][J];
+  ux = (v[1][J] - v[2][J] + v[7][J] + v[8][J] - v[9][J] - v[10][J] + v[11][J] + v[12][J] - v[13][J] - v[14][J]) / r;
+  uy = (v[3][J] - v[4][J] + v[7][J] - v[8][J] + v[9][J] - v[10][J] + v[15][J] - v[16][J] + v[17][J] - v[18][J]) / r;
+  uz = (v[5][J] - v[6][J] + v[11][J] - v[12][J] + v[13][J] - v[14][J] + v[15][J] + v[16][J] - v[17][J] - v[18][J]) / r;
+  rho = r;
+  relax4_fast<J>(v, tau, y, r, ux, uy, uz, AllQ{});
+}
 
 template <int F, int MINW = 1, int WPB = 4>
 __global__ __launch_bounds__(WPB * 64, MINW) void k_var(const MainArgs a, int ch0) {
@@ -51,10 +75,18 @@ __global__ __launch_bounds__(WPB * 64, MINW) void k_var(const MainArgs a, int ch
       }
     }
     float r0, r1, r2, r3, x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
-    collide_cell<0>(v, a.tau, r0, x0, y0, z0);
-    collide_cell<1>(v, a.tau, r1, x1, y1, z1);
-    collide_cell<2>(v, a.tau, r2, x2, y2, z2);
-    collide_cell<3>(v, a.tau, r3, x3, y3, z3);
+    if constexpr (F & F_FASTDIV) {
+      const float y = 1.0f / a.tau;
+      collide_cell_fast<0>(v, a.tau, y, r0, x0, y0, z0);
+      collide_cell_fast<1>(v, a.tau, y, r1, x1, y1, z1);
+      collide_cell_fast<2>(v, a.tau, y, r2, x2, y2, z2);
+      collide_cell_fast<3>(v, a.tau, y, r3, x3, y3, z3);
+    } else {
+      collide_cell<0>(v, a.tau, r0, x0, y0, z0);
+      collide_cell<1>(v, a.tau, r1, x1, y1, z1);
+      collide_cell<2>(v, a.tau, r2, x2, y2, z2);
+      collide_cell<3>(v, a.tau, r3, x3, y3, z3);
+    }
     const f4 R{r0, r1, r2, r3}, UX{x0, x1, x2, x3}, UY{y0, y1, y2, y3}, UZ{z0, z1, z2, z3};
     unsigned store = 0;
 #pragma unroll
@@ -79,7 +111,7 @@ __global__ __launch_bounds__(WPB * 64, MINW) void k_var(const MainArgs a, int ch
       }
     }
     float* d = a.dst + aidx(c, 0);
-    if (store == 0xfu) {
+    if (store == 0xfu || ((F & F_FULLSTORE) && store)) {
 #pragma unroll
       for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));
       if (a.store_all_macros) {
@@ -187,6 +219,11 @@ int main(int argc, char** argv) {
       VAR("- range mask", F_ALL & ~F_MASK, 1, 4),
       VAR("bare (none)", 0, 1, 4),
       VAR("- list - stop", F_ALL & ~(F_LIST | F_STOP), 1, 4),
+      VAR("full fastdiv", F_ALL | F_FASTDIV, 1, 4),
+      VAR("bare fastdiv", F_FASTDIV, 1, 4),
+      VAR("full fullstore", F_ALL | F_FULLSTORE, 1, 4),
+      VAR("full fullstore fastdiv", F_ALL | F_FULLSTORE | F_FASTDIV, 1, 4),
+      VAR("bare fullstore", F_FULLSTORE, 1, 4),
       VAR("full wpb1", F_ALL, 1, 1),
       VAR("full wpb2", F_ALL, 1, 2),
       VAR("full lb4", F_ALL, 4, 4),
