@@ -76,9 +76,9 @@ typedef struct {
   int device;              /* HIP device ordinal */
   int z_offset;            /* global z of local plane 0 */
   int nz_global;           /* global z extent (== nz for a single-domain run) */
-  /* Row alignment of the device layout: 1..4 = store cell x at x + (x_align - 1); 0 = choose
-   * it from geo so that most rows start their fluid run on a 4-cell boundary.  Slabs of one
-   * lattice must use the same value (lbm_attach_rccl / lbm_group_step check it). */
+  /* Row alignment of the device layout: 1..4 = store cell x at slot x - (x_align - 1) of its
+   * row; 0 = choose it from geo so that most rows start their fluid run on a 4-cell boundary.
+   * Slabs of one lattice must use the same value (lbm_attach_rccl / lbm_group_step check). */
   int x_align;
 } lbm_desc;
 
@@ -130,6 +130,14 @@ int lbm_profile(lbm_ctx* ctx, int enabled);
 int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
 /* The same split by kernel: kind 0 = fused stream-collide, 1 = boundary fix-up. */
 int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
+/* Arithmetic of the relaxation's division by tau (the reference divides, ldc.cu:326-363):
+ * fast_div = 1 when the 3-instruction correctly rounded quotient is in use (tau verified
+ * exhaustively at lbm_create; LBM_EXACT_DIV=1 in the environment forces the compiler's
+ * division).  A wave whose populations leave the quotient's proven domain (|f| outside
+ * [2^-60, 2^40) or |u| >= 2^10, e.g. a diverging run) is re-done with the exact division in
+ * the same step; retried_chunks counts those 256-cell chunks since creation.  Results are
+ * bit-identical either way. */
+int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (re-done by the boundary
  * fix-up kernel each step). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);

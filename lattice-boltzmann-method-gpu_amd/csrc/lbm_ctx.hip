@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,6 +42,9 @@ struct Range {            // one launch range of cells [c_lo, c_hi) with its wor
   float4* prev = nullptr; // their (rho, u) of the previous step
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
+  int* retry = nullptr;   // fast-quotient domain misses: queued chunk ids (capacity nchunks)
+  int* retry_cnt = nullptr;  // two counters, by step parity
+  int fix_blocks = 0, retry_blocks = 0;
 };
 }  // namespace
 
@@ -69,6 +73,8 @@ struct lbm_ctx {
   bool halo_primed = false;
   int64_t n_box = 0, n_fluid = 0, n_slow = 0, n_wall_adj = 0;
   float tau = 0.f, omc = 0.f;
+  bool fast_div = false;  // tau verified for the 3-VALU correctly rounded division
+  unsigned long long* retried = nullptr;  // device: chunks re-done on the exact path
   // profiling
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -109,11 +115,19 @@ struct lbm_ctx {
 namespace {
 
 int64_t cell_of(const Layout& L, int x, int y, int z) {  // local z (storage plane z+1)
-  return (int64_t)(x + L.xoff) + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
+  return (int64_t)(x - L.xshift) + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
 }
 
-// x offset that puts the most common first-fluid x of a row at a multiple of 4
-int choose_xoff(const lbm_desc& d) {
+// copy one raster row into storage, dropping the (outer, passive) cells the shift puts
+// before cell 0 (row 0 of storage plane 0 only)
+template <class T>
+void put_row(std::vector<T>& h, int64_t at, const T* row, int nx) {
+  const int skip = at < 0 ? (int)-at : 0;
+  if (skip < nx) std::memcpy(&h[at + skip], row + skip, sizeof(T) * (nx - skip));
+}
+
+// row shift that puts the most common first-fluid x of a row at a multiple of 4
+int choose_xshift(const lbm_desc& d) {
   if (d.x_align > 0) return d.x_align - 1;
   if (!d.geo) return 2;  // device-generated cavity: fluid starts at x = 2 (ldc.cu:469)
   const int8_t fluid = d.case_kind == LBM_CASE_LDC ? 3 : 4;
@@ -127,8 +141,7 @@ int choose_xoff(const lbm_desc& d) {
         break;
       }
   }
-  const int best = (int)(std::max_element(hist, hist + 4) - hist);
-  return (4 - best) & 3;
+  return (int)(std::max_element(hist, hist + 4) - hist);
 }
 
 // time one kernel launch with HIP events on its own stream (lbm_profile)
@@ -174,8 +187,8 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
   const float* src = c->buf[hstep & 1];
   float* dst = c->buf[(hstep + 1) & 1];
   const int* stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
+  MainArgs a{};
   if (r.nchunks > 0) {
-    MainArgs a{};
     a.src = src; a.dst = dst; a.type = c->type; a.links = c->links;
     a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
     a.partial = r.part;
@@ -183,11 +196,15 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
     a.pitch = c->L.pitch; a.plane = c->L.plane;
     a.c_lo = r.c_lo; a.c_hi = r.c_hi;
     a.tau = c->tau;
+    a.tau_rcp = 1.0f / c->tau;
+    a.fast_div = c->fast_div ? 1 : 0;
+    a.retry = r.retry;
+    a.retry_count = r.retry_cnt ? r.retry_cnt + (hstep & 1) : nullptr;
     a.store_all_macros = store_all ? 1 : 0;
     a.stopped = stopped;
     RCK(timed(c, st, 0, [&] { return launch_main(a, st); }));
   }
-  if (r.nslow > 0) {
+  if (r.fix_blocks + r.retry_blocks > 0) {
     FixArgs f{};
     f.src = src; f.dst = dst; f.type = c->type; f.links = c->links;
     f.rho = c->rho; f.ux = c->ux; f.uy = c->uy; f.uz = c->uz;
@@ -198,6 +215,13 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
     f.store_all_macros = store_all ? 1 : 0;
     f.partial = r.part + (r.nchunks > 0 ? main_grid(r.nchunks) : 0);
     f.stopped = stopped;
+    f.fix_blocks = r.fix_blocks;
+    f.retry_blocks = r.retry_blocks;
+    f.main = a;
+    f.retry = r.retry;
+    f.retry_count = a.retry_count;
+    f.retry_reset = r.retry_cnt ? r.retry_cnt + ((hstep + 1) & 1) : nullptr;
+    f.retried_total = c->retried;
     RCK(timed(c, st, 1, [&] { return launch_fix(f, st); }));
   }
   return LBM_OK;
@@ -230,7 +254,14 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMalloc(&r.prev, sizeof(float4) * r.nslow));
     HIPCK(c, hipMemset(r.prev, 0, sizeof(float4) * r.nslow));
   }
-  r.npart = (r.nchunks ? main_grid(r.nchunks) : 0) + (r.nslow ? fix_grid(r.nslow) : 0);
+  r.fix_blocks = r.nslow ? fix_grid(r.nslow) : 0;
+  if (c->fast_div && r.nchunks) {
+    r.retry_blocks = kRetryBlocks;
+    HIPCK(c, hipMalloc(&r.retry, sizeof(int) * r.nchunks));
+    HIPCK(c, hipMalloc(&r.retry_cnt, sizeof(int) * 2));
+    HIPCK(c, hipMemset(r.retry_cnt, 0, sizeof(int) * 2));
+  }
+  r.npart = (r.nchunks ? main_grid(r.nchunks) : 0) + r.fix_blocks + r.retry_blocks;
   return LBM_OK;
 }
 
@@ -238,6 +269,8 @@ void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
+  if (r.retry) (void)hipFree(r.retry);
+  if (r.retry_cnt) (void)hipFree(r.retry_cnt);
   r = Range{};
 }
 
@@ -258,8 +291,10 @@ int reset_state(lbm_ctx* c) {
   cs.stag_max = host.stag_max;
   cs.tol = host.tol;
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
-  for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid})
+  for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid}) {
     if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
+    if (r->retry_cnt) HIPCK(c, hipMemset(r->retry_cnt, 0, sizeof(int) * 2));
+  }
   if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
     HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->s_comp));
     HIPCK(c, hipStreamSynchronize(c->s_comp));
@@ -301,11 +336,15 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   if (c->d.nz_global <= 0) c->d.nz_global = d.nz;
   c->tau = d.tau;
   c->omc = 1.0f - 1.0f / d.tau;  // the reference's (1.0f - 1.0f / tau), evaluated in fp32
+  {
+    const char* ex = std::getenv("LBM_EXACT_DIV");  // A/B switch: force the compiler's division
+    c->fast_div = !(ex && ex[0] == '1') && verify_fast_div(d.tau);
+  }
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
-  L.xoff = choose_xoff(d);
-  L.pitch = (d.nx + L.xoff + 3) / 4 * 4;
+  L.xshift = choose_xshift(d);
+  L.pitch = (d.nx + 3) / 4 * 4;
   L.planes = d.nz + 2;
   L.plane = (int64_t)L.pitch * L.ny;
   L.ncell = (L.plane * L.planes + kChunk - 1) / kChunk * kChunk;
@@ -349,6 +388,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     CK(hipMalloc(p, sizeof(float) * L.ncell));
     CK(hipMemsetAsync(*p, 0, sizeof(float) * L.ncell, c->s_comp));
   }
+  CK(hipMalloc(&c->retried, sizeof(unsigned long long)));
+  CK(hipMemsetAsync(c->retried, 0, sizeof(unsigned long long), c->s_comp));
   CK(hipMalloc(&c->conv, sizeof(ConvState)));
   CK(hipMemsetAsync(c->conv, 0, sizeof(ConvState), c->s_comp));
   CK(hipMalloc(&c->scratch, sizeof(double) * kReduceBlocks));
@@ -373,11 +414,11 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     const int zlo = d.halo_planes ? -1 : 0, zhi = d.halo_planes ? d.nz + 1 : d.nz;
     for (int z = zlo; z < zhi; ++z)
       for (int y = 0; y < d.ny; ++y)
-        std::memcpy(&h[cell_of(L, 0, y, z)], desc->geo + ((int64_t)(z - zlo) * d.ny + y) * d.nx, d.nx);
+        put_row(h, cell_of(L, 0, y, z), desc->geo + ((int64_t)(z - zlo) * d.ny + y) * d.nx, d.nx);
     CK(hipMemcpyAsync(dcodes, h.data(), L.ncell, hipMemcpyHostToDevice, c->s_comp));
     CK(hipStreamSynchronize(c->s_comp));
   } else {
-    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.xoff, L.plane, L.ncell, d.z_offset, c->d.nz_global,
+    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.xshift, L.plane, L.ncell, d.z_offset, c->d.nz_global,
                         c->s_comp));
   }
   const int64_t ntab = (int64_t)d.nx * c->d.nz_global;
@@ -394,7 +435,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   g.rho = c->rho; g.ux = c->ux; g.uy = c->uy; g.uz = c->uz;
   g.inlet_uy = din; g.outlet_uy = dout;
   g.case_kind = d.case_kind; g.lid_u = d.lid_u;
-  g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.xoff = L.xoff; g.plane = L.plane; g.ncell = L.ncell;
+  g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.xshift = L.xshift; g.planes = L.planes; g.plane = L.plane; g.ncell = L.ncell;
   g.z_offset = d.z_offset; g.nz_global = c->d.nz_global;
   CK(launch_classify(g, c->s_comp));
   CK(launch_flag_fluid(g, c->s_comp));
@@ -456,6 +497,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->partial_all) (void)hipFree(c->partial_all);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
+  if (c->retried) (void)hipFree(c->retried);
   if (c->qsets) (void)hipFree(c->qsets);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->ev_edge, c->ev_halo, c->ev_sum, c->ev_fin})
@@ -492,7 +534,7 @@ int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux
 int lbm_init_ldc(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
-  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.ny, c->d.lid_u, c->s_comp));
+  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.xshift, c->L.ny, c->d.lid_u, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -511,6 +553,17 @@ int lbm_set_f(lbm_ctx* c, const float* f) {
   for (int b = 0; b < 2; ++b)
     HIPCK(c, hipMemcpy(c->buf[b], h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
   return reset_state(c);
+}
+
+int lbm_get_numerics(lbm_ctx* c, int* fast_div, int64_t* retried_chunks) {
+  if (!c) return LBM_ERR_ARG;
+  HIPCK(c, hipSetDevice(c->d.device));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  unsigned long long n = 0;
+  HIPCK(c, hipMemcpy(&n, c->retried, sizeof(n), hipMemcpyDeviceToHost));
+  if (fast_div) *fast_div = c->fast_div ? 1 : 0;
+  if (retried_chunks) *retried_chunks = (int64_t)n;
+  return LBM_OK;
 }
 
 int lbm_set_convergence(lbm_ctx* c, int enabled, int max_it, int stag_max, float tol) {
@@ -783,7 +836,7 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
   c->rank = rank;
   c->nranks = nranks;
   {  // every slab must use the same row layout: the halo planes are copied cell for cell
-    int h[2] = {c->L.pitch * 4 + c->L.xoff, -(c->L.pitch * 4 + c->L.xoff)};
+    int h[2] = {c->L.pitch * 4 + c->L.xshift, -(c->L.pitch * 4 + c->L.xshift)};
     int* dv = nullptr;
     HIPCK(c, hipMalloc(&dv, sizeof(h)));
     HIPCK(c, hipMemcpy(dv, h, sizeof(h), hipMemcpyHostToDevice));
@@ -829,7 +882,7 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   if (!cs || n < 1 || nsteps < 0) return LBM_ERR_ARG;
   lbm_ctx* c0 = cs[0];
   for (int i = 0; i < n; ++i) {
-    if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xoff != c0->L.xoff || cs[i]->L.ny != c0->L.ny ||
+    if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xshift != c0->L.xshift || cs[i]->L.ny != c0->L.ny ||
         cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled || cs[i]->comm) {
       c0->err = "lbm_group_step: slabs must share device, row layout (nx, ny, x_align) and step count, "
                 "without convergence control or RCCL";

@@ -23,10 +23,13 @@ __host__ __device__ __forceinline__ int64_t aidx(int64_t c, int q) {
 
 struct Layout {
   int nx, ny, nz;
-  int xoff;           // storage x = x + xoff: puts the first fluid cell of a row at a
-                      // multiple of 4, so fluid 4-cell lane groups hold no wall cells
-                      // (those groups store whole 16-B vectors; see k_stream_collide)
-  int pitch;          // >= nx + xoff, multiple of 4
+  int xshift;         // cell (x, y, zs) lives at x - xshift + y*pitch + zs*plane: puts the
+                      // first fluid cell of a row on a multiple of 4, so fluid 4-cell lane
+                      // groups hold no wall cells and store whole 16-B vectors (see
+                      // k_stream_collide).  The first xshift cells of a row sit at the end
+                      // of the previous row's slots (pitch >= nx keeps them distinct), so
+                      // x +- 1 stays c +- 1 and a 512-wide row still fills two chunks.
+  int pitch;          // >= nx, multiple of 4
   int planes;         // nz + 2
   int64_t plane;      // pitch * ny
   int64_t ncell;      // plane * planes rounded up to a whole chunk
@@ -53,9 +56,21 @@ struct MainArgs {
   int64_t plane;
   int64_t c_lo, c_hi;   // cell range of this launch (cells outside are not touched)
   float tau;
+  float tau_rcp;        // RN(1 / tau)
+  int fast_div;         // 1: tau passed verify_fast_div (3-VALU correctly rounded x / tau)
+  int* retry;           // fast_div: chunks whose wave left the fast quotient's domain ...
+  int* retry_count;     // ... and their count (re-done exactly by the fix-up launch)
   int store_all_macros;
   const int* stopped;   // nullable
 };
+
+// True when k_stream_collide's fast quotient (q0 = x*y, q = fma(fma(-q0, tau, x), y, q0),
+// y = RN(1/tau)) equals RN(x / tau) for every float x in [1, 2) -- and so, by exact
+// power-of-two scaling, for every |x| in [2^-100, 2^100].  Exhaustive over the binade
+// (8.4 M values, a few ms on the host).
+bool verify_fast_div(float tau);
+
+constexpr int kRetryBlocks = 32;  // fix-up blocks that re-do queued chunks (grid-stride)
 
 // NEE-adjacent fluid cells, one per thread: wall bounce-back and NEE by mask,
 // overwriting what the main kernel stored for them.
@@ -72,8 +87,15 @@ struct FixArgs {
   int64_t plane;
   float tau, omc;
   int nee_active, store_all_macros;
-  double* partial;
+  double* partial;      // fix_blocks NEE partials, then retry_blocks retry partials
   const int* stopped;
+  int fix_blocks;       // fix_grid(n), 0 when n == 0
+  int retry_blocks;     // kRetryBlocks with fast_div, else 0
+  MainArgs main;        // the step's main-kernel arguments, for the queued chunks
+  const int* retry;
+  const int* retry_count;
+  int* retry_reset;     // the other step parity's counter, zeroed for the next step
+  unsigned long long* retried_total;  // running count of re-done chunks (lbm_get_numerics)
 };
 
 struct ConvState {      // device-resident reference main-loop state (ldc.cu:613-685)
@@ -122,19 +144,19 @@ struct GeoArgs {
   const float* outlet_uy;
   int case_kind;
   float lid_u;
-  int nx, ny, pitch, xoff;
+  int nx, ny, pitch, xshift, planes;
   int64_t plane, ncell;
   int z_offset, nz_global;
 };
 hipError_t launch_classify(const GeoArgs& g, hipStream_t s);
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s);
-hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xoff, int64_t plane, int64_t ncell, int z_offset,
+hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
                             int nz_global, hipStream_t s);
 
 // initial populations from per-cell fields (nullable -> rho 1, u 0); form 0 = LDC wi form,
 // 1 = expanded; writes both buffers for every cell
 hipError_t launch_init_feq(float* fa, float* fb, int64_t ncell, int form, const float* rho, const float* ux,
                            const float* uy, const float* uz, hipStream_t s);
-hipError_t launch_init_ldc(float* fa, float* fb, int64_t ncell, int pitch, int ny, float lid_u, hipStream_t s);
+hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int ny, float lid_u, hipStream_t s);
 
 }  // namespace lbm

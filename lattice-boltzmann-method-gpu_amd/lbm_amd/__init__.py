@@ -67,7 +67,7 @@ class lbm_desc(C.Structure):
 LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
-    "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells",
+    "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
 ]
 HOST_SYMBOLS = [
@@ -144,6 +144,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_stats": (C.c_int, [P, f64p, i64p, f64p]),
             "lbm_kernel_times": (C.c_int, [P, C.c_int, f64p, i64p]),
             "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
+            "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
@@ -225,7 +226,7 @@ def x_align_for(geo: np.ndarray, case_kind: int) -> int:
     has = g.any(axis=1)
     first = np.argmax(g, axis=1)[has]
     hist = np.bincount(first & 3, minlength=4)
-    return ((4 - int(np.argmax(hist))) & 3) + 1
+    return int(np.argmax(hist)) + 1
 
 
 def initial_fields(case_kind: int, geo: np.ndarray, inlet_uy=None, outlet_uy=None):
@@ -366,6 +367,12 @@ class Lattice:
         ns = C.c_int64()
         self._ck(lbm_lib().lbm_get_boundary_cells(self.h, C.byref(ns)), "lbm_get_boundary_cells")
         return {"n_box": nb.value, "n_fluid": nf.value, "algo_bytes_per_step": by.value, "n_boundary": ns.value}
+
+    def numerics(self):
+        """(fast_div in use, chunks re-done on the exact division path since creation)."""
+        fd, n = C.c_int(), C.c_int64()
+        self._ck(lbm_lib().lbm_get_numerics(self.h, C.byref(fd), C.byref(n)), "lbm_get_numerics")
+        return {"fast_div": bool(fd.value), "retried_chunks": n.value}
 
     def profile(self, enabled: bool = True):
         self._ck(lbm_lib().lbm_profile(self.h, 1 if enabled else 0), "lbm_profile")

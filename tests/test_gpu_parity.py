@@ -55,6 +55,40 @@ def test_ldc_bitwise(gpu, oracle, n, steps):
         assert_residuals(hg, ho)
 
 
+def test_fast_division_domain_retry(gpu, oracle):
+    """Populations outside the fast quotient's proven domain (a tiny f, a huge f) make their
+    waves re-run on the exact-division path in the same step: still bit-identical, and the
+    re-done chunks are counted.  Cells chosen next to the lid (NEE fix-up) and a wall."""
+    from lbm_amd import cases
+    n = 32
+    lat, geo = cases.ldc(n)
+    assert lat.numerics()["fast_div"]
+    o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
+    f = o.f()
+    f[5, 10, n - 3, 9] = 1e-30   # z, y, x: NEE-adjacent row (y = ny-3 next to the lid at ny-2)
+    f[7, 2, 12, 2] = 3e-25       # wall-adjacent corner region
+    f[11, 16, 16, 16] = 1e-38    # interior
+    lat.set_f(f)
+    o.set_f(f)
+    for s in (1, 1, 3):
+        lat.step(s)
+        o.step(s)
+        assert_bitwise(lat, o, geo, 0, "retry")
+    assert lat.numerics()["retried_chunks"] >= 3
+
+
+def test_exact_division_switch(gpu, oracle, monkeypatch):
+    """LBM_EXACT_DIV=1 keeps the compiler's division; results are the same bits."""
+    from lbm_amd import cases
+    monkeypatch.setenv("LBM_EXACT_DIV", "1")
+    lat, geo = cases.ldc(24)
+    assert not lat.numerics()["fast_div"]
+    o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
+    lat.step(30)
+    o.step(30)
+    assert_bitwise(lat, o, geo, 0, "exact div")
+
+
 def test_initial_state_bitwise(gpu, oracle):
     """lbm_init_equilibrium reproduces both reference initialize() forms bit for bit."""
     from lbm_amd import cases

@@ -5,7 +5,10 @@
 // switched off one at a time on a 512^3 LDC-like box (fluid 2..509, walls at 1 and 510).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
 //     -fhip-fp32-correctly-rounded-divide-sqrt -o tools/lab_main tools/lab_main.hip
-#include "../lattice-boltzmann-method-gpu_amd/csrc/lbm_kernels.hip"
+#ifndef LAB_KERNELS
+#define LAB_KERNELS "../lattice-boltzmann-method-gpu_amd/csrc/lbm_kernels.hip"
+#endif
+#include LAB_KERNELS
 
 #include <algorithm>
 #include <cstdio>
@@ -82,10 +85,14 @@ __global__ __launch_bounds__(WPB * 64, MINW) void k_var(const MainArgs a, int ch
       collide_cell_fast<2>(v, a.tau, y, r2, x2, y2, z2);
       collide_cell_fast<3>(v, a.tau, y, r3, x3, y3, z3);
     } else {
-      collide_cell<0>(v, a.tau, r0, x0, y0, z0);
-      collide_cell<1>(v, a.tau, r1, x1, y1, z1);
-      collide_cell<2>(v, a.tau, r2, x2, y2, z2);
-      collide_cell<3>(v, a.tau, r3, x3, y3, z3);
+      moments<0>(v, r0, x0, y0, z0);
+      relax_cell<0, false>(v, a.tau, 0.f, r0, x0, y0, z0, AllQ{});
+      moments<1>(v, r1, x1, y1, z1);
+      relax_cell<1, false>(v, a.tau, 0.f, r1, x1, y1, z1, AllQ{});
+      moments<2>(v, r2, x2, y2, z2);
+      relax_cell<2, false>(v, a.tau, 0.f, r2, x2, y2, z2, AllQ{});
+      moments<3>(v, r3, x3, y3, z3);
+      relax_cell<3, false>(v, a.tau, 0.f, r3, x3, y3, z3, AllQ{});
     }
     const f4 R{r0, r1, r2, r3}, UX{x0, x1, x2, x3}, UY{y0, y1, y2, y3}, UZ{z0, z1, z2, z3};
     unsigned store = 0;
@@ -137,9 +144,42 @@ __global__ __launch_bounds__(WPB * 64, MINW) void k_var(const MainArgs a, int ch
   }
 }
 
-__global__ void k_lab_type(uint8_t* type, uint32_t* links, int n, int pitch, int64_t plane, int64_t ncell) {
+// the shipped per-chunk body, with the kernel's launch bounds as a parameter
+template <bool FAST, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_prod(const MainArgs a, int ch0) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int idx = blockIdx.x * 4 + wave;
+  double acc = 0.0;
+  if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane);
+  const double s = block_sum(acc, red);
+  if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
+}
+
+// the same with the occupancy pinned by amdgpu_waves_per_eu(W, W)
+#define KPRODW(NAME, W)                                                                         \
+  template <bool FAST>                                                                          \
+  __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void NAME(      \
+      const MainArgs a, int ch0) {                                                              \
+    __shared__ double red[4];                                                                   \
+    const int lane = threadIdx.x & 63;                                                          \
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                          \
+    const int idx = blockIdx.x * 4 + wave;                                                      \
+    double acc = 0.0;                                                                           \
+    if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane); \
+    const double s = block_sum(acc, red);                                                       \
+    if (threadIdx.x == 0) a.partial[blockIdx.x] = s;                                            \
+  }
+KPRODW(k_prod_w1, 1)
+KPRODW(k_prod_w2, 2)
+KPRODW(k_prod_w3, 3)
+
+__global__ void k_lab_type(uint8_t* type, uint32_t* links, int n, int pitch, int xoff, int64_t plane,
+                           int64_t ncell) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
-    const int x = (int)(c % pitch), y = (int)((c / pitch) % n), z = (int)(c / plane) - 1;
+    const int64_t u = c + xoff;  // the library's row shift (Layout::xshift)
+    const int x = (int)(u % pitch), y = (int)((u / pitch) % n), z = (int)(u / plane) - 1;
     auto cls = [&](int xx, int yy, int zz) -> uint8_t {
       if (xx < 1 || yy < 1 || zz < 1 || xx > n - 2 || yy > n - 2 || zz > n - 2) return kPassive;
       if (xx == 1 || yy == 1 || zz == 1 || xx == n - 2 || yy == n - 2 || zz == n - 2) return kWall;
@@ -168,9 +208,10 @@ int main(int argc, char** argv) {
   const float amp = argc > 3 ? (float)std::atof(argv[3]) : 1e-4f;  // 0: uniform rest state
   Layout L{};
   L.nx = L.ny = L.nz = N;
-  L.pitch = N;
+  const int xoff = argc > 4 ? std::atoi(argv[4]) : 2;  // row shift (Layout::xshift) for LDC
+  L.pitch = (N + 3) / 4 * 4;
   L.planes = N + 2;
-  L.plane = (int64_t)N * N;
+  L.plane = (int64_t)L.pitch * N;
   L.ncell = (L.plane * L.planes + kChunk - 1) / kChunk * kChunk;
   L.nchunk = L.ncell / kChunk;
   L.guard = (L.plane + L.pitch + 1 + kChunk - 1) / kChunk + 1;
@@ -185,10 +226,14 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&type, L.ncell + 64));
   CK(hipMalloc(&links, sizeof(uint32_t) * (L.ncell + 64)));
   CK(hipMalloc(&stopped, sizeof(int)));
+  int *retry, *retry_cnt;
+  CK(hipMalloc(&retry, sizeof(int) * (N * (int64_t)N * N / 256 + 1024)));
+  CK(hipMalloc(&retry_cnt, sizeof(int)));
+  CK(hipMemset(retry_cnt, 0, sizeof(int)));
   CK(hipMemset(stopped, 0, sizeof(int)));
   hipLaunchKernelGGL(k_lab_fill, dim3(8192), dim3(256), 0, 0, A, L.buf_floats(), amp);
   hipLaunchKernelGGL(k_lab_fill, dim3(8192), dim3(256), 0, 0, B, L.buf_floats(), amp);
-  hipLaunchKernelGGL(k_lab_type, dim3(8192), dim3(256), 0, 0, type, links, N, L.pitch, L.plane, L.ncell);
+  hipLaunchKernelGGL(k_lab_type, dim3(8192), dim3(256), 0, 0, type, links, N, L.pitch, xoff, L.plane, L.ncell);
   // active chunks: storage planes 3 .. N (fluid z 2 .. N-3)
   const int64_t c_lo = 3 * L.plane, c_hi = (int64_t)(N - 1) * L.plane;
   const int ch0 = (int)(c_lo / kChunk), nch = (int)((c_hi - c_lo) / kChunk);
@@ -209,25 +254,21 @@ int main(int argc, char** argv) {
 #define VAR(NAME, F, MINW, WPB)                                                                                  \
   V{NAME, [](const MainArgs& m, int c0, int n) {                                                               \
       hipLaunchKernelGGL((k_var<F, MINW, WPB>), dim3((n + WPB - 1) / WPB), dim3(WPB * 64), 0, 0, m, c0); }}
+#define PROD(NAME, FAST, MINW)                                                                                \
+  V{NAME, [](const MainArgs& m, int c0, int n) {                                                               \
+      hipLaunchKernelGGL((k_prod<FAST, MINW>), dim3((n + 3) / 4), dim3(256), 0, 0, m, c0); }}
   std::vector<V> vs = {
-      VAR("full (production)", F_ALL, 1, 4),
-      VAR("- chunk list", F_ALL & ~F_LIST, 1, 4),
-      VAR("- stopped flag", F_ALL & ~F_STOP, 1, 4),
-      VAR("- block sum", F_ALL & ~F_BSUM, 1, 4),
-      VAR("- |u| accumulate", F_ALL & ~F_UABS, 1, 4),
-      VAR("- bounce-back", F_ALL & ~F_BB, 1, 4),
-      VAR("- range mask", F_ALL & ~F_MASK, 1, 4),
-      VAR("bare (none)", 0, 1, 4),
-      VAR("- list - stop", F_ALL & ~(F_LIST | F_STOP), 1, 4),
-      VAR("full fastdiv", F_ALL | F_FASTDIV, 1, 4),
-      VAR("bare fastdiv", F_FASTDIV, 1, 4),
-      VAR("full fullstore", F_ALL | F_FULLSTORE, 1, 4),
-      VAR("full fullstore fastdiv", F_ALL | F_FULLSTORE | F_FASTDIV, 1, 4),
-      VAR("bare fullstore", F_FULLSTORE, 1, 4),
-      VAR("full wpb1", F_ALL, 1, 1),
-      VAR("full wpb2", F_ALL, 1, 2),
-      VAR("full lb4", F_ALL, 4, 4),
-      VAR("bare lb4", 0, 4, 4),
+#define LDSV(NAME, K, LDS) V{NAME, [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL(K, dim3((n + 3) / 4), dim3(256), LDS, 0, m, c0); }}
+      LDSV("fast lb1 (170 vgpr)", (k_prod<true, 1>), 0),
+      LDSV("fast w2", (k_prod_w2<true>), 0),
+      LDSV("fast w2 lds56k", (k_prod_w2<true>), 56 * 1024),
+      LDSV("exact w2 lds56k", (k_prod_w2<false>), 56 * 1024),
+      LDSV("exact lds56k", (k_prod<false, 1>), 56 * 1024),
+      LDSV("exact (159, occ3)", (k_prod<false, 1>), 0),
+      LDSV("fast lb3 (168, occ3)", (k_prod<true, 3>), 0),
+      LDSV("exact w3", (k_prod_w3<false>), 0),
+      LDSV("fast lb1 (170 vgpr) again", (k_prod<true, 1>), 0),
+      LDSV("exact lds56k again", (k_prod<false, 1>), 56 * 1024),
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -240,6 +281,7 @@ int main(int argc, char** argv) {
       m.rho = mac; m.ux = mac + L.ncell; m.uy = mac + 2 * L.ncell; m.uz = mac + 3 * L.ncell;
       m.partial = part; m.chunks = chunks; m.nchunks = nch; m.pitch = L.pitch; m.plane = L.plane;
       m.c_lo = c_lo; m.c_hi = c_hi; m.tau = 0.55f; m.store_all_macros = 0; m.stopped = stopped;
+      m.tau_rcp = 1.0f / 0.55f; m.fast_div = 1; m.retry = retry; m.retry_count = retry_cnt;
       CK(hipEventRecord(e0));
       for (int it = 0; it < 4; ++it) {
         m.src = (it & 1) ? b_base : a_base;
@@ -254,6 +296,9 @@ int main(int argc, char** argv) {
       ms[i].push_back(t / 4);
     }
   }
+  int nretry = 0;
+  CK(hipMemcpy(&nretry, retry_cnt, sizeof(int), hipMemcpyDeviceToHost));
+  std::printf("retried chunks (all fast launches): %d\n", nretry);
   for (size_t i = 0; i < vs.size(); ++i) {
     std::sort(ms[i].begin(), ms[i].end());
     const float med = ms[i][ms[i].size() / 2];
