@@ -14,9 +14,11 @@ each) overlapped with the interior update plus the residual all-reduce.  Populat
 resident in HBM before timing starts (generated on the device).
 
 Rank 0 prints ONE JSON line.  `value` = MLUPS over all ranks counting NX*NY*NZ box cells
-(SURVEY.md 8(d)); `roofline.achieved` = 152 B x fluid cells per step / average kernel time
-from HIP events recorded on the kernels' own stream; `cpu_baseline` = the serial oracle
-(oracle/, a port of the reference algorithm) on one host core, N = 1 only.
+(SURVEY.md 8(d)); `roofline.achieved` = 152 B x fluid cells / average k_stream_collide
+duration from HIP events recorded on the kernel's own stream; `roofline.traffic` = the
+HBM bytes per launch rocprofv3 counted for the same kernel (profiles/pmc_traffic.json);
+`cpu_baseline` = the serial oracle (oracle/, a port of the reference algorithm) on one
+host core, N = 1 only.
 """
 from __future__ import annotations
 
@@ -55,11 +57,11 @@ def cpu_baseline(n: int = 256, steps: int = 12):
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per launch measured by rocprofv3 PMC passes (tools/pmc_traffic.py writes it)."""
+    """HBM bytes per k_stream_collide launch measured by rocprofv3 PMC passes
+    (tools/gpu_profile.sh + tools/pmc_traffic.py write profiles/pmc_traffic.json)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(p))
-        return d.get(workload, {}).get("bytes_per_launch")
+        return json.load(open(p)).get(workload)
     except (OSError, ValueError):
         return None
 
@@ -147,11 +149,15 @@ def main():
     box_cells = n * n * nzg
     ms_step = elapsed / args.steps * 1e3
     mlups = box_cells * args.steps / elapsed / 1e6
-    # per-rank kernel time per step: stream-collide + boundary fix-up (edge + interior for N > 1)
-    kernel_step_ms = kern_ms / args.steps
-    achieved = BYTES_PER_CELL * counts["n_fluid"] / (kernel_step_ms * 1e-3) / 1e9
+    # dominant kernel: k_stream_collide, timed with HIP events on its own stream; per step it
+    # moves 152 B per fluid cell of the slab (19 fp32 pulls + 19 fp32 stores) -- one launch
+    # at N = 1, three (lo edge, hi edge, interior) per step on a slab at N > 1
+    main_avg_ms = main_ms / main_n
+    main_step_ms = main_ms / args.steps
+    algo_bytes = BYTES_PER_CELL * counts["n_fluid"]
+    achieved = algo_bytes / (main_step_ms * 1e-3) / 1e9
     workload = f"ldc_{n}x{n}x{n}_per_gpu"
-    traffic = pmc_traffic(workload)
+    pmc = pmc_traffic(workload)
     line = {
         "metric": "MLUPS (million lattice updates/sec) + achieved HBM GB/s vs roofline",
         "value": round(mlups, 1),
@@ -177,15 +183,19 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_stream_collide + k_boundary_fixup (one time step; 152 B x fluid cells)",
+            "kernel": "k_stream_collide (fused pull-stream + BGK collide + half-way bounce-back)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algo_bytes_per_launch": BYTES_PER_CELL * counts["n_fluid"],
-            "avg_kernel_ms_per_step": round(kernel_step_ms, 4),
-            "avg_stream_collide_ms": round(main_ms / main_n, 4),
+            "traffic": pmc.get("bytes_per_launch") if pmc else None,
+            "traffic_source": (f"profiles/pmc_traffic.json ({pmc.get('tag')}: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                               f"per launch, 512^3 N=1)") if pmc else None,
+            "algo_bytes_per_launch": algo_bytes,
+            "avg_kernel_ms": round(main_avg_ms, 4),
+            "kernel_ms_per_step": round(main_step_ms, 4),
+            "launches": main_n,
+            "step_kernels_ms": round(kern_ms / args.steps, 4),
             "avg_boundary_fixup_ms_per_step": round(fix_ms / args.steps, 4),
             "boundary_cells_per_gpu": counts["n_boundary"],
         },
