@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 import lbm_amd  # noqa: E402
 from lbm_amd import cases  # noqa: E402
+from lbm_amd import dist as ldist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_CELL = 152    # 19 fp32 loads + 19 fp32 stores per fluid cell update
@@ -96,16 +97,14 @@ def main():
     lbm_amd.require_gpu()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        cpu_group = dist.new_group(backend="gloo")
+        # host-side coordination only (gloo); the data path is liblbm's own RCCL communicator
+        dist.init_process_group("gloo")
 
     n = args.n
     nzg = n * world
     lat = cases.ldc_device(n, n, n, z_offset=rank * n, nz_global=nzg, device=local)
     if world > 1:
-        obj = [lbm_amd.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0, group=cpu_group)
-        lat.attach_rccl(obj[0], rank, world)
+        lat.attach_rccl(ldist.share_unique_id(rank, None, lbm_amd.rccl_unique_id), rank, world)
     counts = lat.counts()
 
     def barrier():
@@ -130,12 +129,8 @@ def main():
     main_ms, main_n = st["stream_collide_ms"], max(1, st["stream_collide_launches"])
     fix_ms = st["boundary_fixup_ms"]
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms, main_ms, fix_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, main_ms, fix_ms = (float(v) for v in t)
-        fl = torch.tensor([counts["n_fluid"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(fl)
-        n_fluid_total = int(fl.item())
+        elapsed, kern_ms, main_ms, fix_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms, fix_ms], None)
+        n_fluid_total = int(ldist.sum_over_ranks([counts["n_fluid"]], None)[0])
     else:
         n_fluid_total = counts["n_fluid"]
     lat.close()

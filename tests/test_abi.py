@@ -1,0 +1,84 @@
+"""The C-ABI boundary (include/*.h): every declared function is exported by the built
+library and bound by the Python mirror; the libraries load on a CPU-only host and fail
+loudly (no CPU fallback) where a device is needed.  No compute runs here."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import PKG, REPO
+
+HEADERS = {
+    "lbm.h": os.path.join(PKG, "lib", "liblbm.so"),
+    "lbm_host.h": os.path.join(PKG, "lib", "liblbm_host.so"),
+}
+DECL = re.compile(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*\b(lbmh?_[a-z0-9_]+)\s*\(", re.M)
+
+
+def declared(header: str):
+    text = open(os.path.join(REPO, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(DECL.findall(text)))
+
+
+def exported(lib: str):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+@pytest.mark.parametrize("header", sorted(HEADERS))
+def test_header_symbols_exported(header):
+    names = declared(header)
+    assert len(names) >= 10
+    lib = HEADERS[header]
+    assert os.path.exists(lib), f"{lib} not built (make -C {PKG})"
+    missing = set(names) - exported(lib)
+    assert not missing, f"{os.path.basename(lib)} lacks {sorted(missing)}"
+
+
+def test_python_mirror_binds_every_symbol(lbm):
+    assert sorted(lbm.LBM_SYMBOLS) == declared("lbm.h")
+    assert sorted(lbm.HOST_SYMBOLS) == declared("lbm_host.h")
+    L, H = lbm.lbm_lib(), lbm.host_lib()
+    for name in lbm.LBM_SYMBOLS:
+        assert getattr(L, name).argtypes is not None, name
+    for name in lbm.HOST_SYMBOLS:
+        assert getattr(H, name).argtypes is not None, name
+
+
+def test_desc_layout_matches_header(lbm):
+    """lbm_desc field order in the ctypes mirror follows include/lbm.h."""
+    text = open(os.path.join(REPO, "include", "lbm.h")).read()
+    body = text[text.index("typedef struct {"):text.index("} lbm_desc;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"\b([a-z_][a-z0-9_]*)\s*(?:,|;)", body)
+    assert [f[0] for f in lbm.lbm_desc._fields_] == fields
+
+
+def test_loads_without_device_and_fails_loudly(lbm):
+    """Version works with no GPU; creating a context without a device is an error with a
+    message -- never a silent CPU fallback."""
+    assert "gfx950" in lbm.version()
+    if lbm.gpu_available():
+        pytest.skip("a device is visible")
+    with pytest.raises(lbm.LbmError, match="hipSetDevice|device"):
+        lbm.Lattice(lbm.LBM_CASE_LDC, (8, 8, 8), 0.55, None)
+    with pytest.raises(lbm.LbmError):
+        lbm.require_gpu()
+
+
+def test_invalid_descriptions_rejected(lbm):
+    with pytest.raises(lbm.LbmError, match="invalid lattice description"):
+        lbm.Lattice(lbm.LBM_CASE_LDC, (8, 8, 2), 0.55, None)  # nx < 3
+    with pytest.raises(lbm.LbmError, match="invalid lattice description"):
+        lbm.Lattice(lbm.LBM_CASE_LDC, (8, 8, 8), -1.0, None)
+    with pytest.raises(lbm.LbmError, match="geo == NULL"):
+        lbm.Lattice(lbm.LBM_CASE_POISEUILLE, (8, 8, 8), 0.58, None)
+    with pytest.raises(lbm.LbmError, match="invalid lattice description"):
+        lbm.Lattice(lbm.LBM_CASE_LDC, (8, 8, 8), 0.55, None, x_align=7)
+
+
+def test_drivers_built():
+    for exe in ("ldc", "poiseuille", "bifurcation"):
+        assert os.access(os.path.join(PKG, "bin", exe), os.X_OK), exe

@@ -1,0 +1,105 @@
+"""The CPU oracle (oracle/, test infrastructure) against its pins and the golden vectors.
+
+* pins.json holds full runs of oracle/pin_check.py against the known answers SURVEY.md
+  records for the reference (oracle/PINNING.md); every recorded value must match.
+* golden.json / golden.npz (tests/golden/make_golden.py) are re-derived here bit for bit.
+* The long convergence pins re-run only with LBM_SLOW=1 (minutes each).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO
+
+PINS = os.path.join(REPO, "oracle", "pins.json")
+SLOW = os.environ.get("LBM_SLOW") == "1"
+
+
+def test_recorded_pins_match_known_answers():
+    pins = json.load(open(PINS))
+    assert set(pins) >= {"geometry", "poiseuille_converge", "ldc_serial_converge", "bif_as_shipped",
+                         "bif_inlet_block1", "ldc_two_phase_converge"}
+    g = pins["geometry"]
+    for k, v in g["expect"].items():
+        assert g[k] == v, k
+    p = pins["poiseuille_converge"]
+    assert p["stop_k"] == 6230 and p["nlattice"] == 214128 and p["fluid"] == 175200
+    assert abs(p["uy_max"] - 0.096993) < 5e-7
+    assert p["bad_reads"] == 0
+    assert pins["ldc_serial_converge"]["stop_k"] == 5335
+    b = pins["bif_as_shipped"]
+    assert abs(b["umax"] - 3.5e-6) < 5e-8
+    b = pins["bif_inlet_block1"]
+    assert abs(b["umax"] - 0.224) < 5e-4
+    assert abs(b["rho_min"] - 0.994) < 5e-4 and abs(b["rho_max"] - 1.141) < 5e-4
+
+
+def test_geometry_pins_live(oracle):
+    n, _ = oracle.index_transform(oracle.geo_poiseuille(64, 64, 64))
+    assert n == 214128
+    raw = oracle.read_geo_txt(os.path.join(GOLDEN, "bifurcation", "geo.txt"), 64, 83, 32)
+    assert int((raw == 1).sum()) == 54388 and int((raw == 0).sum()) == 115596
+    geo = oracle.geo_mask(raw)
+    n, _ = oracle.index_transform(geo)
+    assert n == 65820  # thesis 4.8
+
+
+def _golden_cases():
+    import sys
+    sys.path.insert(0, os.path.join(GOLDEN))
+    import make_golden
+    return make_golden
+
+
+@pytest.mark.parametrize("name", ["ldc16_two_phase", "ldc16_serial", "poiseuille_20x24x20", "bif_inlet_block1"])
+def test_golden_vectors(oracle, name):
+    mg = _golden_cases()
+    meta = json.load(open(os.path.join(GOLDEN, "golden.json")))[name]
+    kind, geo, tau, kw, steps = mg.case_setups()[name]
+    m, (rho, ux, uy, uz, hist) = mg.run(name, kind, geo, tau, kw, steps)
+    for k in ("sha256_macros_fluid", "sha256_f_fluid", "sha256_residuals", "n_fluid", "bad_reads"):
+        assert m[k] == meta[k], (name, k)
+    arrs = np.load(os.path.join(GOLDEN, "golden.npz"))
+    if f"{name}.rho" in arrs:
+        for k, a in zip(("rho", "ux", "uy", "uz"), (rho, ux, uy, uz)):
+            assert np.array_equal(arrs[f"{name}.{k}"].view(np.uint32), a.view(np.uint32))
+
+
+def test_ldc_orders_agree_to_race_noise(oracle):
+    """The two LDC wall orders (two-phase = race-free semantics, serial = one serialisation
+    of the reference's racy in-place bounce-back) differ by race noise: a few percent in the
+    start-up transient measured here, 2e-4 at convergence."""
+    g = oracle.geo_ldc(16, 16, 16)
+    a = oracle.Oracle(oracle.LDC, g, 0.55, ldc_order=oracle.TWO_PHASE)
+    b = oracle.Oracle(oracle.LDC, g, 0.55, ldc_order=oracle.SERIAL_EMU)
+    a.step(40)
+    b.step(40)
+    fl = g == 3
+    ua = np.stack(a.macros()[1:])[:, fl]
+    ub = np.stack(b.macros()[1:])[:, fl]
+    rel = np.linalg.norm(ua - ub) / np.linalg.norm(ua)
+    assert 0 < rel < 5e-2
+
+
+def test_mass_conservation_closed_box(oracle):
+    """Bounce-back walls conserve mass: with the lid at rest the LDC box keeps sum(rho)."""
+    g = oracle.geo_ldc(12, 12, 12)
+    g[g == 2] = 1  # lid -> wall: fully closed box
+    o = oracle.Oracle(oracle.LDC, g, 0.55)
+    o.step(1)
+    m0 = float(o.macros()[0][g == 3].astype(np.float64).sum())
+    o.step(30)
+    m1 = float(o.macros()[0][g == 3].astype(np.float64).sum())
+    assert abs(m1 - m0) / m0 < 1e-6
+
+
+@pytest.mark.skipif(not SLOW, reason="minutes: set LBM_SLOW=1")
+def test_poiseuille_converge_pin(oracle):
+    g = oracle.geo_poiseuille(64, 64, 64)
+    o = oracle.Oracle(oracle.POISEUILLE, g, 0.58)  # the oracle's own uygt, as pin_check.py
+    k, _ = o.run_converge()
+    assert k == 6230
+    uy = o.macros()[2]
+    assert abs(float(uy[g == 4].max()) - 0.096993) < 5e-7
