@@ -299,11 +299,15 @@ __global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int idx = blockIdx.x * (kBlock / 64) + wave;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2),
+  // so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of chunks
+  // and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
+  const int lb = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+  const int idx = lb * (kBlock / 64) + wave;
   double acc = 0.0;
   if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
   const double s = block_sum(acc, red);
-  if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
+  if (threadIdx.x == 0) a.partial[lb] = s;
 }
 
 // ---- boundary fix-up ------------------------------------------------------------------
@@ -647,7 +651,8 @@ bool verify_fast_div(float tau) {
   return true;
 }
 
-int main_grid(int nchunks) { return std::max(1, (nchunks + kBlock / 64 - 1) / (kBlock / 64)); }
+// blocks of the main kernel: a multiple of the 8 XCDs (see k_stream_collide)
+int main_grid(int nchunks) { return std::max(8, ((nchunks + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8); }
 int fix_grid(int n) { return std::max(1, (n + 255) / 256); }
 
 // Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one):

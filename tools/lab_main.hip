@@ -157,6 +157,22 @@ __global__ __launch_bounds__(256, MINW) void k_prod(const MainArgs a, int ch0) {
   if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
 }
 
+// XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so logical block
+// (b % 8) * (nb / 8) + b / 8 gives every XCD (its own L2) one contiguous run of chunks
+template <bool FAST>
+__global__ __launch_bounds__(256) void k_prod_xcd(const MainArgs a, int ch0) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nb = gridDim.x;  // multiple of 8
+  const int lb = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+  const int idx = lb * 4 + wave;
+  double acc = 0.0;
+  if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane);
+  const double s = block_sum(acc, red);
+  if (threadIdx.x == 0) a.partial[lb] = s;
+}
+
 // the same with the occupancy pinned by amdgpu_waves_per_eu(W, W)
 #define KPRODW(NAME, W)                                                                         \
   template <bool FAST>                                                                          \
@@ -259,7 +275,11 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((k_prod<FAST, MINW>), dim3((n + 3) / 4), dim3(256), 0, 0, m, c0); }}
   std::vector<V> vs = {
 #define LDSV(NAME, K, LDS) V{NAME, [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL(K, dim3((n + 3) / 4), dim3(256), LDS, 0, m, c0); }}
+      V{"SHIPPED k_stream_collide", [](const MainArgs& m, int c0, int n) { (void)c0; (void)n; (void)launch_main(m, 0); }},
       LDSV("fast lb1 (170 vgpr)", (k_prod<true, 1>), 0),
+      V{"fast xcd lds56k", [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL((k_prod_xcd<true>), dim3(((n + 3) / 4 + 7) / 8 * 8), dim3(256), 56 * 1024, 0, m, c0); }},
+      V{"exact xcd lds56k", [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL((k_prod_xcd<false>), dim3(((n + 3) / 4 + 7) / 8 * 8), dim3(256), 56 * 1024, 0, m, c0); }},
+      LDSV("fast lds56k", (k_prod<true, 1>), 56 * 1024),
       LDSV("fast w2", (k_prod_w2<true>), 0),
       LDSV("fast w2 lds56k", (k_prod_w2<true>), 56 * 1024),
       LDSV("exact w2 lds56k", (k_prod_w2<false>), 56 * 1024),
