@@ -33,8 +33,8 @@ std::string g_create_error;
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
-struct Range {            // one launch range of cells [c_lo, c_hi) with its work lists
-  int64_t c_lo = 0, c_hi = 0;
+struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) with their work lists
+  int64_t c_lo = 0, c_hi = 0, c_lo2 = 0, c_hi2 = 0;
   int* chunks = nullptr;  // active 256-cell chunks (>= 1 fluid cell in range)
   int nchunks = 0;
   int* cells = nullptr;   // NEE-adjacent fluid cells
@@ -58,7 +58,7 @@ struct lbm_ctx {
   uint8_t* type = nullptr;
   uint32_t* links = nullptr;
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
-  Range whole, lo, hi, mid;  // single domain: whole; slabs: lo edge, hi edge, interior
+  Range whole, edge, mid;  // single domain: whole; slabs: both edge planes (one launch), interior
   double* partial_all = nullptr;
   int npart_slab = 0;
   double* scratch = nullptr;
@@ -194,7 +194,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
     a.partial = r.part;
     a.chunks = r.chunks; a.nchunks = r.nchunks;
     a.pitch = c->L.pitch; a.plane = c->L.plane;
-    a.c_lo = r.c_lo; a.c_hi = r.c_hi;
+    a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
     a.tau = c->tau;
     a.tau_rcp = 1.0f / c->tau;
     a.fast_div = c->fast_div ? 1 : 0;
@@ -227,21 +227,32 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
   return LBM_OK;
 }
 
-// work lists of the cell range [lo, hi) from the host copy of the type bytes
-int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t) {
+// work lists of the cells [lo, hi) u [lo2, hi2) from the host copy of the type bytes
+int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t, int64_t lo2 = 0,
+                int64_t hi2 = 0) {
+  if (lo2 < hi) lo2 = hi2 = 0;  // overlapping second interval (single-plane slab): drop it
   r.c_lo = lo;
   r.c_hi = hi;
+  r.c_lo2 = lo2;
+  r.c_hi2 = hi2;
   std::vector<int> chunks, cells;
-  for (int64_t ch = lo / kChunk; ch * kChunk < hi; ++ch) {
-    bool any = false;
-    for (int64_t k = std::max(lo, ch * kChunk); k < std::min(hi, (ch + 1) * kChunk); ++k) {
-      const uint8_t v = t[k];
-      if ((v & kClassMask) != kFluid) continue;
-      any = true;
-      if (v & kNeedsMac) cells.push_back((int)k);
+  auto in = [&](int64_t k) { return (k >= lo && k < hi) || (k >= lo2 && k < hi2); };
+  auto scan = [&](int64_t a, int64_t b) {
+    for (int64_t ch = a / kChunk; ch * kChunk < b; ++ch) {
+      if (!chunks.empty() && chunks.back() >= (int)ch) continue;  // chunk shared by both intervals
+      bool any = false;
+      for (int64_t k = ch * kChunk; k < (ch + 1) * kChunk; ++k) {
+        if (!in(k)) continue;
+        const uint8_t v = t[k];
+        if ((v & kClassMask) != kFluid) continue;
+        any = true;
+        if (v & kNeedsMac) cells.push_back((int)k);
+      }
+      if (any) chunks.push_back((int)ch);
     }
-    if (any) chunks.push_back((int)ch);
-  }
+  };
+  scan(lo, hi);
+  if (hi2 > lo2) scan(lo2, hi2);
   r.nchunks = (int)chunks.size();
   r.nslow = (int)cells.size();
   if (r.nchunks) {
@@ -291,7 +302,7 @@ int reset_state(lbm_ctx* c) {
   cs.stag_max = host.stag_max;
   cs.tol = host.tol;
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
-  for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid}) {
+  for (Range* r : {&c->whole, &c->edge, &c->mid}) {
     if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
     if (r->retry_cnt) HIPCK(c, hipMemset(r->retry_cnt, 0, sizeof(int) * 2));
   }
@@ -466,16 +477,14 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     c->n_fluid = nf;
     const int64_t P = L.plane, nz = d.nz;
     if (build_range(c, c->whole, P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
-    if (build_range(c, c->lo, P, 2 * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
-    if (nz > 1 && build_range(c, c->hi, nz * P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);
     if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t) != LBM_OK) return bail(LBM_ERR_HIP);
     // partial slots: [whole | lo | hi | mid]; the slab ranges are contiguous
-    c->npart_slab = c->lo.npart + c->hi.npart + c->mid.npart;
+    c->npart_slab = c->edge.npart + c->mid.npart;
     CK(hipMalloc(&c->partial_all, sizeof(double) * std::max(1, c->whole.npart + c->npart_slab)));
     c->whole.part = c->partial_all;
-    c->lo.part = c->whole.part + c->whole.npart;
-    c->hi.part = c->lo.part + c->lo.npart;
-    c->mid.part = c->hi.part + c->hi.npart;
+    c->edge.part = c->whole.part + c->whole.npart;
+    c->mid.part = c->edge.part + c->edge.npart;
   }
 #undef CK
   *out = c;
@@ -491,7 +500,7 @@ void lbm_destroy(lbm_ctx* c) {
   for (float* p : {c->alloc[0], c->alloc[1], c->rho, c->ux, c->uy, c->uz, c->hist, c->send_up, c->send_dn,
                    c->recv_up, c->recv_dn})
     if (p) (void)hipFree(p);
-  for (Range* r : {&c->whole, &c->lo, &c->hi, &c->mid}) free_range(*r);
+  for (Range* r : {&c->whole, &c->edge, &c->mid}) free_range(*r);
   if (c->type) (void)hipFree(c->type);
   if (c->links) (void)hipFree(c->links);
   if (c->partial_all) (void)hipFree(c->partial_all);
@@ -666,11 +675,12 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
     // edge planes first, so their halo travels while the interior runs
-    RCK(run_range(c, c->lo, h, store_all, c->s_comp));
-    if (c->L.nz > 1) RCK(run_range(c, c->hi, h, store_all, c->s_comp));
+    RCK(run_range(c, c->edge, h, store_all, c->s_comp));
     RCK(rccl_exchange(c, (h + 1) & 1, false));
     RCK(run_range(c, c->mid, h, store_all, c->s_comp));
-    HIPCK(c, launch_reduce(c->lo.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp));
+    // the previous step's all-reduce has read s_local / the finisher has run
+    HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
+    HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp));
     HIPCK(c, hipEventRecord(c->ev_sum, c->s_comp));
     HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_sum, 0));
     NCCK(c, ncclAllReduce(&c->conv->s_local, &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
@@ -910,10 +920,9 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     const bool store_all = (s == nsteps - 1);
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      RCK(run_range(c, c->lo, h, store_all, st));
-      if (c->L.nz > 1) RCK(run_range(c, c->hi, h, store_all, st));
+      RCK(run_range(c, c->edge, h, store_all, st));
       RCK(run_range(c, c->mid, h, store_all, st));
-      HIPCK(c, launch_reduce(c->lo.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
+      HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
     }
     RCK(loopback_exchange(cs, n, (h + 1) & 1, false, st));
     hipLaunchKernelGGL(k_sum_locals, dim3(1), dim3(1), 0, st, dconvs, n);

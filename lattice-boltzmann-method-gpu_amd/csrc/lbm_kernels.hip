@@ -238,7 +238,8 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   for (int j = 0; j < 4; ++j) {
     const unsigned t = (t4 >> (8 * j)) & 0xffu;
     const int64_t cj = c + j;
-    const bool in = cj >= a.c_lo && cj < a.c_hi && (t & kClassMask) == kFluid && !(RETRY && (t & kNeedsMac));
+    const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
+                    !(RETRY && (t & kNeedsMac));
     if (in) {
       store |= 1u << j;
       if (!(t & kNeedsMac)) acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
@@ -246,12 +247,13 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
   // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
-  // bounce-back slots / boundary data and cells outside [c_lo, c_hi) belong to another
+  // bounce-back slots / boundary data and cells outside the launch's ranges belong to another
   // launch, so those lanes store cell by cell -- sub-16-B stores cost whole partial-line
   // writes in HBM (the x-ends of every row took 15% of the step before the xshift alignment).
   const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
   const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
-  const bool keep_others = special != 0u || c < a.c_lo || c + 4 > a.c_hi ||
+  const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
+  const bool keep_others = special != 0u || !lane_in ||
                            (RETRY && (t4 & (kNeedsMac * 0x01010101u)));
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
   if (a.store_all_macros) {

@@ -54,7 +54,9 @@ struct MainArgs {
   int nchunks;
   int pitch;
   int64_t plane;
-  int64_t c_lo, c_hi;   // cell range of this launch (cells outside are not touched)
+  int64_t c_lo, c_hi;   // cell ranges of this launch, [c_lo, c_hi) and [c_lo2, c_hi2) (the
+  int64_t c_lo2, c_hi2; // second one empty except for a slab's two edge planes); cells
+                        // outside them are not touched
   float tau;
   float tau_rcp;        // RN(1 / tau)
   int fast_div;         // 1: tau passed verify_fast_div (3-VALU correctly rounded x / tau)
