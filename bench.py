@@ -14,7 +14,7 @@ each) overlapped with the interior update plus the residual all-reduce.  Populat
 resident in HBM before timing starts (generated on the device).
 
 Rank 0 prints ONE JSON line.  `value` = MLUPS over all ranks counting NX*NY*NZ box cells
-(SURVEY.md 8(d)); `roofline.achieved` = 152 B x fluid cells / average k_stream_collide
+(SURVEY.md 8(d)); `roofline.achieved` = 152 B x fluid cells / average k_step
 duration from HIP events recorded on the kernel's own stream; `roofline.traffic` = the
 HBM bytes per launch rocprofv3 counted for the same kernel (profiles/pmc_traffic.json);
 `cpu_baseline` = the serial oracle (oracle/, a port of the reference algorithm) on one
@@ -58,7 +58,7 @@ def cpu_baseline(n: int = 256, steps: int = 12):
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per k_stream_collide launch measured by rocprofv3 PMC passes
+    """HBM bytes per k_step launch measured by rocprofv3 PMC passes
     (tools/gpu_profile.sh + tools/pmc_traffic.py write profiles/pmc_traffic.json)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -103,7 +103,7 @@ def perturbed_mlups(n: int, steps: int, dev: int):
     st = lat.stats()
     lat.close()
     return {"mlups": round(n ** 3 * steps / dt / 1e6, 1),
-            "avg_kernel_ms": round(st["stream_collide_ms"] / max(1, st["stream_collide_launches"]), 4)}
+            "avg_kernel_ms": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]), 4)}
 
 
 def main():
@@ -153,10 +153,9 @@ def main():
     state = lat.state()
     elapsed = t1 - t0
     kern_ms = st["kernel_ms"]
-    main_ms, main_n = st["stream_collide_ms"], max(1, st["stream_collide_launches"])
-    fix_ms = st["boundary_fixup_ms"]
+    main_ms, main_n = st["step_kernel_ms"], max(1, st["step_kernel_launches"])
     if world > 1:
-        elapsed, kern_ms, main_ms, fix_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms, fix_ms], None)
+        elapsed, kern_ms, main_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms], None)
         n_fluid_total = int(ldist.sum_over_ranks([counts["n_fluid"]], None)[0])
     else:
         n_fluid_total = counts["n_fluid"]
@@ -171,9 +170,9 @@ def main():
     box_cells = n * n * nzg
     ms_step = elapsed / args.steps * 1e3
     mlups = box_cells * args.steps / elapsed / 1e6
-    # dominant kernel: k_stream_collide, timed with HIP events on its own stream; per step it
-    # moves 152 B per fluid cell of the slab (19 fp32 pulls + 19 fp32 stores) -- one launch
-    # at N = 1, three (lo edge, hi edge, interior) per step on a slab at N > 1
+    # dominant kernel: k_step, timed with HIP events on its own stream; per step it moves
+    # 152 B per fluid cell of the slab (19 fp32 pulls + 19 fp32 stores) -- one launch at
+    # N = 1, two (both edge planes, then the interior) per step on a slab at N > 1
     main_avg_ms = main_ms / main_n
     main_step_ms = main_ms / args.steps
     algo_bytes = BYTES_PER_CELL * counts["n_fluid"]
@@ -205,7 +204,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_stream_collide (fused pull-stream + BGK collide + half-way bounce-back)",
+            "kernel": "k_step (fused pull-stream + BGK collide + half-way bounce-back + NEE cells)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -217,8 +216,6 @@ def main():
             "avg_kernel_ms": round(main_avg_ms, 4),
             "kernel_ms_per_step": round(main_step_ms, 4),
             "launches": main_n,
-            "step_kernels_ms": round(kern_ms / args.steps, 4),
-            "avg_boundary_fixup_ms_per_step": round(fix_ms / args.steps, 4),
             "boundary_cells_per_gpu": counts["n_boundary"],
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},

@@ -123,12 +123,13 @@ int lbm_get_f(lbm_ctx* ctx, float* f_soa);
  * (152 B per fluid cell: 19 fp32 loads + 19 fp32 stores). */
 int lbm_get_counts(lbm_ctx* ctx, int64_t* n_box, int64_t* n_fluid, double* algo_bytes_per_step);
 
-/* Kernel timing: when enabled, HIP events bracket every collide-stream launch on the
- * stream it runs on; lbm_stats returns the summed kernel milliseconds and launch count
- * since enabling. */
+/* Kernel timing: when enabled, HIP events bracket every step-kernel launch on the stream it
+ * runs on; lbm_stats returns the summed kernel milliseconds and launch count since enabling. */
 int lbm_profile(lbm_ctx* ctx, int enabled);
 int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
-/* The same split by kernel: kind 0 = fused stream-collide, 1 = boundary fix-up. */
+/* The same for one kind of launch: kind 0 = the step kernel (k_step: stream-collide with
+ * bounce-back and the NEE-adjacent cells, one launch per step and launch range); kind 1 is
+ * reserved (0 launches). */
 int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
 /* Arithmetic of the relaxation's division by tau (the reference divides, ldc.cu:326-363):
  * fast_div = 1 when the 3-instruction correctly rounded quotient is in use (tau verified
@@ -138,8 +139,8 @@ int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
  * the same step; retried_chunks counts those 256-cell chunks since creation.  Results are
  * bit-identical either way. */
 int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
-/* Fluid cells next to a non-equilibrium-extrapolation boundary (re-done by the boundary
- * fix-up kernel each step). */
+/* Fluid cells next to a non-equilibrium-extrapolation boundary (done by the NEE blocks of
+ * the step kernel). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
 
 /* Multi-GPU z-slabs (one process per GPU).  Rank 0 calls lbm_rccl_unique_id, the 128 bytes

@@ -43,8 +43,8 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
   int* retry = nullptr;   // fast-quotient domain misses: queued chunk ids (capacity nchunks)
-  int* retry_cnt = nullptr;  // two counters, by step parity
-  int fix_blocks = 0, retry_blocks = 0;
+  int* retry_cnt = nullptr;  // their count (emptied by the reduction launch)
+  int main_blocks = 0, nee_blocks = 0;
 };
 }  // namespace
 
@@ -180,56 +180,39 @@ int harvest_profile(lbm_ctx* c) {
   return LBM_OK;
 }
 
-// one step's update of a range: main kernel over the active chunks, then the boundary
-// fix-up of the listed cells (same stream: the fix-up overwrites what the main kernel stored)
-int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st) {
-  const bool first = (hstep == 0);
-  const float* src = c->buf[hstep & 1];
-  float* dst = c->buf[(hstep + 1) & 1];
-  const int* stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
+// one step's update of a range: ONE k_step launch (chunk blocks + NEE-adjacent cell blocks).
+// allow_fast = false keeps the exact division (slab edges: their halo is packed right after,
+// before the reduction that would re-do queued chunks).  *out: the arguments, for the
+// reduction's retry pass.
+int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, bool allow_fast = true,
+              MainArgs* out = nullptr) {
   MainArgs a{};
-  if (r.nchunks > 0) {
-    a.src = src; a.dst = dst; a.type = c->type; a.links = c->links;
-    a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
-    a.partial = r.part;
-    a.chunks = r.chunks; a.nchunks = r.nchunks;
-    a.pitch = c->L.pitch; a.plane = c->L.plane;
-    a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
-    a.tau = c->tau;
-    a.tau_rcp = 1.0f / c->tau;
-    a.fast_div = c->fast_div ? 1 : 0;
-    a.retry = r.retry;
-    a.retry_count = r.retry_cnt ? r.retry_cnt + (hstep & 1) : nullptr;
-    a.store_all_macros = store_all ? 1 : 0;
-    a.stopped = stopped;
-    RCK(timed(c, st, 0, [&] { return launch_main(a, st); }));
-  }
-  if (r.fix_blocks + r.retry_blocks > 0) {
-    FixArgs f{};
-    f.src = src; f.dst = dst; f.type = c->type; f.links = c->links;
-    f.rho = c->rho; f.ux = c->ux; f.uy = c->uy; f.uz = c->uz;
-    f.prev = r.prev; f.cells = r.cells; f.n = r.nslow;
-    f.pitch = c->L.pitch; f.plane = c->L.plane;
-    f.tau = c->tau; f.omc = c->omc;
-    f.nee_active = first ? 0 : 1;
-    f.store_all_macros = store_all ? 1 : 0;
-    f.partial = r.part + (r.nchunks > 0 ? main_grid(r.nchunks) : 0);
-    f.stopped = stopped;
-    f.fix_blocks = r.fix_blocks;
-    f.retry_blocks = r.retry_blocks;
-    f.main = a;
-    f.retry = r.retry;
-    f.retry_count = a.retry_count;
-    f.retry_reset = r.retry_cnt ? r.retry_cnt + ((hstep + 1) & 1) : nullptr;
-    f.retried_total = c->retried;
-    RCK(timed(c, st, 1, [&] { return launch_fix(f, st); }));
-  }
+  a.src = c->buf[hstep & 1];
+  a.dst = c->buf[(hstep + 1) & 1];
+  a.type = c->type; a.links = c->links;
+  a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
+  a.partial = r.part;
+  a.chunks = r.chunks; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks;
+  a.pitch = c->L.pitch; a.plane = c->L.plane;
+  a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
+  a.tau = c->tau;
+  a.tau_rcp = 1.0f / c->tau;
+  a.fast_div = (c->fast_div && allow_fast && r.retry) ? 1 : 0;
+  a.retry = r.retry;
+  a.retry_count = a.fast_div ? r.retry_cnt : nullptr;
+  a.store_all_macros = store_all ? 1 : 0;
+  a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
+  a.cells = r.cells; a.prev = r.prev; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
+  a.nee_active = hstep == 0 ? 0 : 1;
+  a.omc = c->omc;
+  if (out) *out = a;
+  if (r.main_blocks + r.nee_blocks > 0) RCK(timed(c, st, 0, [&] { return launch_step(a, st); }));
   return LBM_OK;
 }
 
 // work lists of the cells [lo, hi) u [lo2, hi2) from the host copy of the type bytes
 int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t, int64_t lo2 = 0,
-                int64_t hi2 = 0) {
+                int64_t hi2 = 0, bool with_retry = true) {
   if (lo2 < hi) lo2 = hi2 = 0;  // overlapping second interval (single-plane slab): drop it
   r.c_lo = lo;
   r.c_hi = hi;
@@ -265,14 +248,14 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMalloc(&r.prev, sizeof(float4) * r.nslow));
     HIPCK(c, hipMemset(r.prev, 0, sizeof(float4) * r.nslow));
   }
-  r.fix_blocks = r.nslow ? fix_grid(r.nslow) : 0;
-  if (c->fast_div && r.nchunks) {
-    r.retry_blocks = kRetryBlocks;
+  r.main_blocks = main_grid(r.nchunks);
+  r.nee_blocks = nee_grid(r.nslow);
+  if (c->fast_div && r.nchunks && with_retry) {
     HIPCK(c, hipMalloc(&r.retry, sizeof(int) * r.nchunks));
-    HIPCK(c, hipMalloc(&r.retry_cnt, sizeof(int) * 2));
-    HIPCK(c, hipMemset(r.retry_cnt, 0, sizeof(int) * 2));
+    HIPCK(c, hipMalloc(&r.retry_cnt, sizeof(int)));
+    HIPCK(c, hipMemset(r.retry_cnt, 0, sizeof(int)));
   }
-  r.npart = (r.nchunks ? main_grid(r.nchunks) : 0) + r.fix_blocks + r.retry_blocks;
+  r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }
 
@@ -304,7 +287,7 @@ int reset_state(lbm_ctx* c) {
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
   for (Range* r : {&c->whole, &c->edge, &c->mid}) {
     if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
-    if (r->retry_cnt) HIPCK(c, hipMemset(r->retry_cnt, 0, sizeof(int) * 2));
+    if (r->retry_cnt) HIPCK(c, hipMemset(r->retry_cnt, 0, sizeof(int)));
   }
   if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
     HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->s_comp));
@@ -403,7 +386,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   CK(hipMemsetAsync(c->retried, 0, sizeof(unsigned long long), c->s_comp));
   CK(hipMalloc(&c->conv, sizeof(ConvState)));
   CK(hipMemsetAsync(c->conv, 0, sizeof(ConvState), c->s_comp));
-  CK(hipMalloc(&c->scratch, sizeof(double) * kReduceBlocks));
+  CK(hipMalloc(&c->scratch, sizeof(double) * 2 * kReduceBlocks));
   {
     int h[29];
     for (int k = 0; k < 5; ++k) {
@@ -477,7 +460,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     c->n_fluid = nf;
     const int64_t P = L.plane, nz = d.nz;
     if (build_range(c, c->whole, P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
-    if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P, false) != LBM_OK) return bail(LBM_ERR_HIP);
     if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t) != LBM_OK) return bail(LBM_ERR_HIP);
     // partial slots: [whole | lo | hi | mid]; the slab ranges are contiguous
     c->npart_slab = c->edge.npart + c->mid.npart;
@@ -656,9 +639,10 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
   int h = c->steps_done;
   for (int s = 0; s < nsteps; ++s, ++h) {
     const bool store_all = c->conv_enabled || (s == nsteps - 1);
-    RCK(run_range(c, c->whole, h, store_all, c->s_comp));
+    MainArgs a{};
+    RCK(run_range(c, c->whole, h, store_all, c->s_comp, true, &a));
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
-                           1, c->s_comp));
+                           1, a.fast_div ? &a : nullptr, c->retried, c->s_comp));
   }
   return LBM_OK;
 }
@@ -675,12 +659,14 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
     // edge planes first, so their halo travels while the interior runs
-    RCK(run_range(c, c->edge, h, store_all, c->s_comp));
+    MainArgs a{};
+    RCK(run_range(c, c->edge, h, store_all, c->s_comp, false));
     RCK(rccl_exchange(c, (h + 1) & 1, false));
-    RCK(run_range(c, c->mid, h, store_all, c->s_comp));
+    RCK(run_range(c, c->mid, h, store_all, c->s_comp, true, &a));
     // the previous step's all-reduce has read s_local / the finisher has run
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
-    HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp));
+    HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, a.fast_div ? &a : nullptr,
+                           c->retried, c->s_comp));
     HIPCK(c, hipEventRecord(c->ev_sum, c->s_comp));
     HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_sum, 0));
     NCCK(c, ncclAllReduce(&c->conv->s_local, &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
@@ -920,9 +906,11 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     const bool store_all = (s == nsteps - 1);
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      RCK(run_range(c, c->edge, h, store_all, st));
-      RCK(run_range(c, c->mid, h, store_all, st));
-      HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
+      MainArgs a{};
+      RCK(run_range(c, c->edge, h, store_all, st, false));
+      RCK(run_range(c, c->mid, h, store_all, st, true, &a));
+      HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, a.fast_div ? &a : nullptr,
+                             c->retried, st));
     }
     RCK(loopback_exchange(cs, n, (h + 1) & 1, false, st));
     hipLaunchKernelGGL(k_sum_locals, dim3(1), dim3(1), 0, st, dconvs, n);

@@ -1,27 +1,28 @@
 // lbm_kernels.hip -- CDNA4 (gfx950) kernels of the D3Q19 BGK hot path.
 //
 // The reference's per-step kernels update + boundary_stream + calc_vel_square
-// (ldc.cu:57-466, Poiseulle.cu:384-901, bifurcation.cu:429-1023) become:
+// (ldc.cu:57-466, Poiseulle.cu:384-901, bifurcation.cu:429-1023) become one launch of
+// k_step per launch range plus the reduction:
 //
-//  k_stream_collide  one wavefront per 256-cell AoSoA chunk, 4 consecutive cells per
-//                    lane: 19 aligned 16-B pulls (x neighbours by a DPP lane shift, the two
-//                    edge lanes read one extra float), moments, equilibria and BGK
-//                    relaxation in registers, 19 16-B stores into the chunk.
-//                    Half-way bounce-back costs no extra pass and no extra round trip:
-//                    a wall-adjacent cell also stores its outgoing population opp(q) into
-//                    the slot q of the wall it pulls q from next step (producer side; the
-//                    value Poiseulle.cu:601-746 / ldc.cu:184-201 write there), so every
+//  k_step, chunk blocks  one wavefront per 256-cell AoSoA chunk, 4 consecutive cells per
+//                    lane: 19 aligned 16-B pulls issued at once (x neighbours by a DPP lane
+//                    shift, the edge lanes' floats by wave-uniform scalar loads), moments,
+//                    equilibria and BGK relaxation in registers, 19 16-B stores into the
+//                    chunk.  Half-way bounce-back costs no extra pass and no extra round
+//                    trip: a wall-adjacent cell also stores its outgoing population opp(q)
+//                    into the slot q of the wall it pulls q from next step (producer side;
+//                    the value Poiseulle.cu:601-746 / ldc.cu:184-201 write there), so every
 //                    pull is a plain load.
-//  k_boundary_fixup  one thread per fluid cell next to an NEE cell (a compact list of
-//                    contiguous rows, ~0.2% of the cells at 512^3): re-does the cell and
-//                    overwrites it, with
+//  k_step, NEE blocks    one thread per fluid cell next to an NEE cell (a compact list,
+//                    ~0.2% of the cells at 512^3), which the chunk blocks leave alone:
 //                      NEE cell B at c - e_q with e_q . n_B = 1:
 //                        f_q = feq_q(rho_bc, u_bc) + (src[q][c] - feq_q(rho_c, u_c)) (1 - 1/tau)
 //                        with the cell's own (rho, u) of the previous step (the value
 //                        boundary_stream writes into B, ldc.cu:391-456, Poiseulle.cu:748-891,
 //                        bifurcation.cu:877-1021; their hand-simplified "tmp" terms are
 //                        bit-identical to feq_q(rho_bc, u_bc)).
-//  k_reduce_*        deterministic two-level sum of the per-block |u| partials and the
+//  k_reduce_*        deterministic two-level sum of the per-block |u| partials (and any
+//                    chunk the fast division path queued, re-done exactly) and the
 //                    residual / convergence logic of ldc.cu:660-684 on the device.
 // HBM traffic per fluid cell: 76 B loaded + 76 B stored + 1 B type.
 #include <cmath>
@@ -191,13 +192,12 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
   return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f;  // false for NaN
 }
 
-// One wave's chunk: pull, collide, store; returns the lane's |u| sum.
-//  FAST:  the 3-VALU quotient when the whole wave lies in its domain; a wave that does not
-//         stores nothing and queues its chunk for the exact path (both paths in one kernel
-//         would cost a third of the registers: 232 vs 168).
-//  RETRY: the exact path run for queued chunks inside the boundary fix-up launch, which
-//         concurrently re-does the NEE-adjacent cells: those are left to it.
-template <bool FAST, bool RETRY>
+// One wave's chunk: pull, collide, store; returns the lane's |u| sum.  NEE-adjacent cells
+// are left to the NEE blocks of the same launch (nee_cell).
+//  FAST: the 3-VALU quotient when the whole wave lies in its domain; a wave that does not
+//        stores nothing and queues its chunk for the exact path, run by the reduction
+//        launch (both paths in one kernel would cost a third of the registers: 232 vs 168).
+template <bool FAST>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane) {
   double acc = 0.0;
   const int64_t c = cb + lane * 4;
@@ -239,10 +239,10 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     const unsigned t = (t4 >> (8 * j)) & 0xffu;
     const int64_t cj = c + j;
     const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
-                    !(RETRY && (t & kNeedsMac));
+                    !(t & kNeedsMac);
     if (in) {
       store |= 1u << j;
-      if (!(t & kNeedsMac)) acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
+      acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
     }
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
@@ -253,8 +253,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
   const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
-  const bool keep_others = special != 0u || !lane_in ||
-                           (RETRY && (t4 & (kNeedsMac * 0x01010101u)));
+  const bool keep_others = special != 0u || !lane_in || (t4 & (kNeedsMac * 0x01010101u));
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
   if (a.store_all_macros) {
     if (whole) {
@@ -295,31 +294,14 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   return acc;
 }
 
-template <bool FAST>
-__global__ __launch_bounds__(kBlock) void k_stream_collide(const MainArgs a) {
-  __shared__ double red[kBlock / 64];
-  if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2),
-  // so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of chunks
-  // and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
-  const int lb = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
-  const int idx = lb * (kBlock / 64) + wave;
-  double acc = 0.0;
-  if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
-  const double s = block_sum(acc, red);
-  if (threadIdx.x == 0) a.partial[lb] = s;
-}
-
-// ---- boundary fix-up ------------------------------------------------------------------
+// ---- NEE-adjacent cells ----------------------------------------------------------------
 
 struct Macro {
   float rho, ux, uy, uz;
 };
 
 template <int Q>
-__device__ __forceinline__ void fix_pull(float* f, const FixArgs& a, int64_t c, const Macro& mp) {
+__device__ __forceinline__ void fix_pull(float* f, const MainArgs& a, int64_t c, const Macro& mp) {
   const int64_t nb = c - (Dir<Q>::x + row_off<Q>(a.pitch, a.plane));
   f[Q] = a.src[aidx(nb, Q)];
   if constexpr (Q == 0) return;
@@ -344,7 +326,7 @@ __device__ __forceinline__ void fix_pull(float* f, const FixArgs& a, int64_t c, 
 }
 
 template <int... Qs>
-__device__ __forceinline__ void fix_pull_all(float* f, const FixArgs& a, int64_t c, const Macro& mp,
+__device__ __forceinline__ void fix_pull_all(float* f, const MainArgs& a, int64_t c, const Macro& mp,
                                              std::integer_sequence<int, Qs...>) {
   (fix_pull<Qs>(f, a, c, mp), ...);
 }
@@ -361,48 +343,57 @@ __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict_
   if (m) (bb_store_one<Qs>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
 }
 
-__global__ __launch_bounds__(256) void k_boundary_fixup(const FixArgs a) {
-  __shared__ double red[4];
-  if (a.stopped != nullptr && *a.stopped) return;
+// One NEE-adjacent fluid cell (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021
+// applied on the consumer side): its pulls with the NEE value substituted for every
+// population an NEE neighbour supplies, collide (exact division), store incl. its own
+// bounce-back slots, keep its (rho, u) for the next step's NEE values.
+__device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
+  const int64_t c = a.cells[i];
+  const float4 pv = a.prev[i];
+  const Macro mp{pv.x, pv.y, pv.z, pv.w};
+  float f[kQ];
+  fix_pull_all(f, a, c, mp, AllQ{});
+  float rho = 0.f;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) rho = rho + f[q];
+  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
+  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
+  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
+  fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
+  fix_store_all(f, a.dst, c, a.links[c], a.pitch, a.plane, AllQ{});
+  a.prev[i] = make_float4(rho, ux, uy, uz);
+  if (a.store_all_macros) {
+    a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
+  }
+  return (double)sqrtf(ux * ux + uy * uy + uz * uz);
+}
+
+// ---- the step kernel -------------------------------------------------------------------
+
+template <bool FAST>
+__global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
+  __shared__ double red[kBlock / 64];
+  if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
   double acc = 0.0;
-  if ((int)blockIdx.x >= a.fix_blocks) {  // chunks the fast main kernel queued: exact path
-    const int n = *a.retry_count;
-    if (blockIdx.x == a.fix_blocks && threadIdx.x == 0) {
-      *a.retry_reset = 0;  // next step's queue
-      if (n) atomicAdd(a.retried_total, (unsigned long long)n);
-    }
+  int slot;
+  if ((int)blockIdx.x >= a.nee_blocks) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int stride = (gridDim.x - a.fix_blocks) * 4;
-    for (int k = ((int)blockIdx.x - a.fix_blocks) * 4 + wave; k < n; k += stride)
-      acc += process_chunk<false, true>(a.main, (int64_t)a.retry[k] * kChunk, lane);
-    const double s = block_sum(acc, red);
-    if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
-    return;
-  }
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.n) {
-    const int64_t c = a.cells[i];
-    const float4 pv = a.prev[i];
-    const Macro mp{pv.x, pv.y, pv.z, pv.w};
-    float f[kQ];
-    fix_pull_all(f, a, c, mp, AllQ{});
-    float rho = 0.f;
-#pragma unroll
-    for (int q = 0; q < kQ; ++q) rho = rho + f[q];
-    const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
-    const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
-    const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-    fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
-    fix_store_all(f, a.dst, c, a.links[c], a.pitch, a.plane, AllQ{});
-    a.prev[i] = make_float4(rho, ux, uy, uz);
-    if (a.store_all_macros) {
-      a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
-    }
-    acc = (double)sqrtf(ux * ux + uy * uy + uz * uz);
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own
+    // L2), so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of
+    // chunks and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
+    const int b = (int)blockIdx.x - a.nee_blocks;  // nee_blocks is a multiple of 8
+    slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
+    const int idx = slot * (kBlock / 64) + wave;
+    if (idx < a.nchunks) acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
+    slot += a.nee_blocks;
+  } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
+    slot = blockIdx.x;
+    const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+    if (i < a.n_nee) acc = nee_cell(a, i);
   }
   const double s = block_sum(acc, red);
-  if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
+  if (threadIdx.x == 0) a.partial[slot] = s;
 }
 
 // ---- residual --------------------------------------------------------------------------
@@ -419,8 +410,11 @@ __device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
   if (hist_slot) *hist_slot = residual;
 }
 
+// slice b of the block partials -> out[b]; then the chunks the fast path queued, re-done
+// with the exact division by all slice blocks together -> out[gridDim.x + b]
 __global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict__ partial, int n,
-                                                       double* __restrict__ out, const ConvState* cv) {
+                                                       double* __restrict__ out, const ConvState* cv,
+                                                       const MainArgs m, int retry) {
   __shared__ double red[4];
   if (cv->stopped) return;
   const int len = (n + gridDim.x - 1) / gridDim.x;
@@ -429,17 +423,37 @@ __global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict_
   for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s += partial[i];
   s = block_sum(s, red);
   if (threadIdx.x == 0) out[blockIdx.x] = s;
+  double r = 0.0;
+  if (retry) {
+    const int nq = *m.retry_count;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int k = (int)blockIdx.x * 4 + wave; k < nq; k += (int)gridDim.x * 4)
+      r += process_chunk<false>(m, (int64_t)m.retry[k] * kChunk, lane);
+  }
+  __syncthreads();  // red[] reuse
+  r = block_sum(r, red);
+  if (threadIdx.x == 0) out[gridDim.x + blockIdx.x] = r;
 }
 
 __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__ slices, int n, ConvState* cv,
-                                                      float* hist_slot, int finish) {
+                                                      float* hist_slot, int finish, int* retry_count,
+                                                      unsigned long long* retried_total) {
   __shared__ double red[4];
   if (cv->stopped) return;
-  double s = threadIdx.x < n ? slices[threadIdx.x] : 0.0;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += slices[i];  // fixed order
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
     cv->s_local = s;
     if (finish) residual_logic(cv, s, hist_slot);
+    if (retry_count) {
+      const int nq = *retry_count;
+      if (nq) {
+        *retried_total += (unsigned long long)nq;
+        *retry_count = 0;
+      }
+    }
   }
 }
 
@@ -653,32 +667,35 @@ bool verify_fast_div(float tau) {
   return true;
 }
 
-// blocks of the main kernel: a multiple of the 8 XCDs (see k_stream_collide)
-int main_grid(int nchunks) { return std::max(8, ((nchunks + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8); }
-int fix_grid(int n) { return std::max(1, (n + 255) / 256); }
+// chunk blocks of k_step: a multiple of the 8 XCDs (see k_step)
+int main_grid(int nchunks) {
+  return nchunks ? std::max(8, ((nchunks + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
+}
+// NEE blocks of k_step (first in the grid): a multiple of 8 so the chunk blocks keep their XCD
+int nee_grid(int n) { return (n + 8 * kBlock - 1) / (8 * kBlock) * 8; }
 
 // Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one):
 // a 56-KB dynamic LDS reservation caps every CU at two of these 4-wave blocks whatever the
 // register count the compiler settles on.
 constexpr size_t kOccupancyLds = 56 * 1024;
 
-hipError_t launch_main(const MainArgs& a, hipStream_t s) {
+hipError_t launch_step(const MainArgs& a, hipStream_t s) {
+  const dim3 grid(a.main_blocks + a.nee_blocks);
   if (a.fast_div)
-    hipLaunchKernelGGL(k_stream_collide<true>, dim3(main_grid(a.nchunks)), dim3(kBlock), kOccupancyLds, s, a);
+    hipLaunchKernelGGL(k_step<true>, grid, dim3(kBlock), kOccupancyLds, s, a);
   else
-    hipLaunchKernelGGL(k_stream_collide<false>, dim3(main_grid(a.nchunks)), dim3(kBlock), kOccupancyLds, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_fix(const FixArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_boundary_fixup, dim3(a.fix_blocks + a.retry_blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_step<false>, grid, dim3(kBlock), kOccupancyLds, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot, int finish,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv);
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, kReduceBlocks, conv, hist_slot, finish);
+                         const MainArgs* retry, unsigned long long* retried_total, hipStream_t s) {
+  MainArgs m{};
+  if (retry) m = *retry;
+  const int do_retry = (retry && retry->retry_count) ? 1 : 0;
+  hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv, m, do_retry);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, 2 * kReduceBlocks, conv, hist_slot, finish,
+                     do_retry ? retry->retry_count : nullptr, retried_total);
   return hipGetLastError();
 }
 

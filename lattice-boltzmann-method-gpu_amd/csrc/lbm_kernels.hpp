@@ -40,18 +40,25 @@ struct Layout {
   int64_t buf_floats() const { return (nchunk + 2 * guard) * kQ * kChunk; }
 };
 
-// Fused pull-stream + BGK collide over a list of chunks, treating every neighbour as a
-// plain pull; stores fluid cells; |u| partials of fluid cells that are not slow.
+// One time step of one launch range, ONE kernel launch (k_step):
+//  * blocks [0, nee_blocks): one thread per NEE-adjacent fluid cell, done with the NEE
+//    values of its boundary neighbours (and its own bounce-back slots);
+//  * blocks [nee_blocks, nee_blocks + main_blocks): fused pull-stream + BGK collide, one
+//    wavefront per active 256-cell chunk, every neighbour a plain pull, wall bounce-back
+//    stored producer-side; stores every fluid cell of the range except the NEE-adjacent
+//    ones -- disjoint cells, so both parts run concurrently.
+// Partials: one fp64 |u| sum per block (NEE blocks first).
 struct MainArgs {
   const float* src;     // base (past the guard chunk)
   float* dst;
   const uint8_t* type;  // per cell
   const uint32_t* links;  // per cell: bit q set when c - e_q is a wall (read for kWallAdj cells)
                           // -> producer-side bounce-back stores
-  float* rho; float* ux; float* uy; float* uz;
+  float* rho; float* ux; float* uy; float* uz;  // full fields; NEE data sits at NEE cells
   double* partial;      // one per block
   const int* chunks;    // active chunk ids
   int nchunks;
+  int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
   int pitch;
   int64_t plane;
   int64_t c_lo, c_hi;   // cell ranges of this launch, [c_lo, c_hi) and [c_lo2, c_hi2) (the
@@ -61,44 +68,23 @@ struct MainArgs {
   float tau_rcp;        // RN(1 / tau)
   int fast_div;         // 1: tau passed verify_fast_div (3-VALU correctly rounded x / tau)
   int* retry;           // fast_div: chunks whose wave left the fast quotient's domain ...
-  int* retry_count;     // ... and their count (re-done exactly by the fix-up launch)
+  int* retry_count;     // ... and their count (re-done exactly by the reduction launch)
   int store_all_macros;
   const int* stopped;   // nullable
+  // NEE-adjacent fluid cells
+  const int* cells;     // linear ids
+  float4* prev;         // per cell: its (rho, ux, uy, uz) of the previous step
+  int n_nee;
+  int nee_blocks;       // multiple of 8 (keeps the chunk blocks' XCD order)
+  int nee_active;       // 0 at step 0: NEE cells are pulled raw (boundary_stream has not run)
+  float omc;            // the reference's (1.0f - 1.0f / tau)
 };
 
-// True when k_stream_collide's fast quotient (q0 = x*y, q = fma(fma(-q0, tau, x), y, q0),
+// True when k_step's fast quotient (q0 = x*y, q = fma(fma(-q0, tau, x), y, q0),
 // y = RN(1/tau)) equals RN(x / tau) for every float x in [1, 2) -- and so, by exact
 // power-of-two scaling, for every |x| in [2^-100, 2^100].  Exhaustive over the binade
 // (8.4 M values, a few ms on the host).
 bool verify_fast_div(float tau);
-
-constexpr int kRetryBlocks = 32;  // fix-up blocks that re-do queued chunks (grid-stride)
-
-// NEE-adjacent fluid cells, one per thread: wall bounce-back and NEE by mask,
-// overwriting what the main kernel stored for them.
-struct FixArgs {
-  const float* src;
-  float* dst;
-  const uint8_t* type;
-  const uint32_t* links;
-  float* rho; float* ux; float* uy; float* uz;  // full fields; NEE data sits at NEE cells
-  float4* prev;         // per slow cell: its (rho, ux, uy, uz) of the previous step
-  const int* cells;     // slow cell ids (linear)
-  int n;
-  int pitch;
-  int64_t plane;
-  float tau, omc;
-  int nee_active, store_all_macros;
-  double* partial;      // fix_blocks NEE partials, then retry_blocks retry partials
-  const int* stopped;
-  int fix_blocks;       // fix_grid(n), 0 when n == 0
-  int retry_blocks;     // kRetryBlocks with fast_div, else 0
-  MainArgs main;        // the step's main-kernel arguments, for the queued chunks
-  const int* retry;
-  const int* retry_count;
-  int* retry_reset;     // the other step parity's counter, zeroed for the next step
-  unsigned long long* retried_total;  // running count of re-done chunks (lbm_get_numerics)
-};
 
 struct ConvState {      // device-resident reference main-loop state (ldc.cu:613-685)
   double s_local;       // this rank's sum of |u| for the last step
@@ -114,16 +100,17 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
   int pad;
 };
 
-hipError_t launch_main(const MainArgs& a, hipStream_t s);
-hipError_t launch_fix(const FixArgs& a, hipStream_t s);
+hipError_t launch_step(const MainArgs& a, hipStream_t s);
 int main_grid(int nchunks);
-int fix_grid(int n);
+int nee_grid(int n);
 constexpr int kReduceBlocks = 256;
 // partial sums -> conv->s_local (deterministic two-level tree: kReduceBlocks blocks sum
 // fixed contiguous slices into scratch, one block sums scratch); finish=1 also runs the
-// residual logic and writes *hist_slot
+// residual logic and writes *hist_slot.  retry (nullable): the step's arguments whose
+// fast_div queue the slice blocks first re-do with the exact division (their |u| sums join
+// the tree); the final block empties the queue and counts it into *retried_total.
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot,
-                         int finish, hipStream_t s);
+                         int finish, const MainArgs* retry, unsigned long long* retried_total, hipStream_t s);
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
 
 // halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack

@@ -24,7 +24,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)                      # lattice-boltzmann-method-gpu_amd/
 LIB = os.path.join(ROOT, "lib")
-LIBLBM = os.path.join(LIB, "liblbm.so")
+LIBLBM = os.environ.get("LBM_LIBRARY") or os.path.join(LIB, "liblbm.so")  # override: A/B builds
 LIBHOST = os.path.join(LIB, "liblbm_host.so")
 
 LBM_CASE_LDC, LBM_CASE_POISEUILLE, LBM_CASE_MASK = 0, 1, 2
@@ -381,7 +381,7 @@ class Lattice:
         ms, n, by = C.c_double(), C.c_int64(), C.c_double()
         self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
         out = {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
-        for kind, name in ((0, "stream_collide"), (1, "boundary_fixup")):
+        for kind, name in ((0, "step_kernel"),):
             m, k = C.c_double(), C.c_int64()
             self._ck(lbm_lib().lbm_kernel_times(self.h, kind, C.byref(m), C.byref(k)), "lbm_kernel_times")
             out[name + "_ms"], out[name + "_launches"] = m.value, k.value

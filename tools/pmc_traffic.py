@@ -21,8 +21,8 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-MAIN = "k_stream_collide"
-FIX = "k_boundary_fixup"
+MAIN = "k_step"
+FIX = "k_reduce_slices"
 
 
 def per_kernel(path, counter):
@@ -74,7 +74,7 @@ def main():
     wl = os.environ.get("LBM_WORKLOAD", "ldc_512x512x512_per_gpu")
     path = os.path.join(prof, "pmc_traffic.json")
     d = json.load(open(path)) if os.path.exists(path) else {}
-    d[wl] = dict(out.get(MAIN, {}), tag=tag, fixup=out.get(FIX),
+    d[wl] = dict(out.get(MAIN, {}), tag=tag, reduce=out.get(FIX),
                  note="FETCH_SIZE x2 (gfx950 half-count of 16-B/lane streaming reads) + WRITE_SIZE, KiB->B; "
                       "separate --pmc passes of bench.py --steps 20 --warmup 5")
     json.dump(d, open(path, "w"), indent=1)
