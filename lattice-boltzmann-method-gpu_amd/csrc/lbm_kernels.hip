@@ -457,6 +457,39 @@ __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__
   }
 }
 
+// small launch ranges (n <= kReduceOneMax partials): the whole reduction, retries included,
+// in one block -- one launch less per step where launches dominate (LDC 64^3: ~26 us/step)
+constexpr int kReduceOneMax = 16384;
+__global__ __launch_bounds__(512) void k_reduce_one(const double* __restrict__ partial, int n, ConvState* cv,
+                                                     float* hist_slot, int finish, const MainArgs m, int retry,
+                                                     unsigned long long* retried_total) {
+  __shared__ double red[8];
+  if (cv->stopped) return;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];  // fixed order
+  s = block_sum(s, red);
+  double r = 0.0;
+  int nq = 0;
+  if (retry) {
+    nq = *m.retry_count;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int k = wave; k < nq; k += (int)(blockDim.x >> 6))
+      r += process_chunk<false>(m, (int64_t)m.retry[k] * kChunk, lane);
+  }
+  __syncthreads();  // red[] reuse
+  r = block_sum(r, red);
+  if (threadIdx.x == 0) {
+    s += r;
+    cv->s_local = s;
+    if (finish) residual_logic(cv, s, hist_slot);
+    if (nq) {
+      *retried_total += (unsigned long long)nq;
+      *m.retry_count = 0;
+    }
+  }
+}
+
 __global__ void k_finish_global(ConvState* cv, float* hist_slot) {
   if (cv->stopped) return;
   residual_logic(cv, cv->s_global, hist_slot);
@@ -693,6 +726,11 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
   MainArgs m{};
   if (retry) m = *retry;
   const int do_retry = (retry && retry->retry_count) ? 1 : 0;
+  if (n <= kReduceOneMax) {
+    hipLaunchKernelGGL(k_reduce_one, dim3(1), dim3(512), 0, s, partial, n, conv, hist_slot, finish, m, do_retry,
+                       retried_total);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv, m, do_retry);
   hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, 2 * kReduceBlocks, conv, hist_slot, finish,
                      do_retry ? retry->retry_count : nullptr, retried_total);

@@ -274,3 +274,24 @@ def test_matches_committed_golden(gpu, name):
     h.update(np.ascontiguousarray(lat.f()[:, fl]).tobytes())
     assert h.hexdigest() == meta["sha256_f_fluid"]
     lbm_amd  # noqa: B018
+
+
+def test_fast_division_retry_large(gpu, oracle):
+    """The same injected out-of-domain populations on LDC 256^3, where the per-block partials
+    exceed the one-block reduction and the re-done chunks go through the sliced reduction."""
+    from lbm_amd import cases
+    n = 256
+    lat, geo = cases.ldc(n)
+    o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
+    f = o.f()
+    f[5, 100, n - 3, 17] = 1e-30
+    f[7, 2, 140, 2] = 3e-25
+    f[11, 200, 60, 201] = 7e-39
+    lat.set_f(f)
+    o.set_f(f)
+    del f
+    for s in (1, 2):
+        lat.step(s, history=False)
+        o.step(s)
+    assert_bitwise(lat, o, geo, 0, "retry 256")
+    assert lat.numerics()["retried_chunks"] >= 3
