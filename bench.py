@@ -79,6 +79,31 @@ def small_case_mlups(n: int, steps: int, dev: int):
     return round(n ** 3 * steps / dt / 1e6, 1)
 
 
+def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
+    lat.step(warm, history=False)
+    lat.sync()
+    t = time.perf_counter()
+    lat.step(steps, history=False)
+    lat.sync()
+    dt = time.perf_counter() - t
+    lat.close()
+    return {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
+
+
+def config_lines(dev: int):
+    """BASELINE configs C3 (Poiseuille 128 x 128 x 512, pipe along y) and C4 (the shipped
+    bifurcation mask) as secondary lines: MLUPS over box cells and over the reference's
+    NLATTICE (stored cells, its metric for sparse cases)."""
+    out = {}
+    lat, geo = cases.poiseuille(128, 512, 128, device=dev)
+    nl, _ = lbm_amd.index_transform(geo)
+    out["poiseuille_128x512x128 (C3)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
+    lat, geo, _, _ = cases.bifurcation(1, device=dev)
+    nl, _ = lbm_amd.index_transform(geo)
+    out["bifurcation_64x83x32 (C4)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 2000)
+    return out
+
+
 def perturbed_mlups(n: int, steps: int, dev: int):
     """LDC n^3 started from equilibria of a random velocity field (|u| ~ 0.01, fixed seed)
     instead of rest: populations then carry full-entropy bit patterns, which costs the
@@ -224,7 +249,8 @@ def main():
     if world == 1 and not args.no_secondary:
         line["secondary"] = {"ldc64_mlups (published config)": small_case_mlups(64, 2000, local),
                              "ldc256_mlups (config C2)": small_case_mlups(256, 200, local),
-                             f"ldc{n}_random_velocity_start": perturbed_mlups(n, 50, local)}
+                             f"ldc{n}_random_velocity_start": perturbed_mlups(n, 50, local),
+                             **config_lines(local)}
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     print(json.dumps(line), flush=True)
