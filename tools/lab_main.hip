@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, MINW) void k_prod(const MainArgs a, int ch0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int idx = blockIdx.x * 4 + wave;
   double acc = 0.0;
-  if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane);
+  if (idx < a.nchunks) acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane);
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
 }
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_prod_xcd(const MainArgs a, int ch0) {
   const int lb = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
   const int idx = lb * 4 + wave;
   double acc = 0.0;
-  if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane);
+  if (idx < a.nchunks) acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane);
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[lb] = s;
 }
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_prod_xcd(const MainArgs a, int ch0) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                          \
     const int idx = blockIdx.x * 4 + wave;                                                      \
     double acc = 0.0;                                                                           \
-    if (idx < a.nchunks) acc = process_chunk<FAST, false>(a, (int64_t)a.chunks[idx] * kChunk, lane); \
+    if (idx < a.nchunks) acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane); \
     const double s = block_sum(acc, red);                                                       \
     if (threadIdx.x == 0) a.partial[blockIdx.x] = s;                                            \
   }
@@ -275,20 +275,13 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((k_prod<FAST, MINW>), dim3((n + 3) / 4), dim3(256), 0, 0, m, c0); }}
   std::vector<V> vs = {
 #define LDSV(NAME, K, LDS) V{NAME, [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL(K, dim3((n + 3) / 4), dim3(256), LDS, 0, m, c0); }}
-      V{"SHIPPED k_stream_collide", [](const MainArgs& m, int c0, int n) { (void)c0; (void)n; (void)launch_main(m, 0); }},
-      LDSV("fast lb1 (170 vgpr)", (k_prod<true, 1>), 0),
-      V{"fast xcd lds56k", [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL((k_prod_xcd<true>), dim3(((n + 3) / 4 + 7) / 8 * 8), dim3(256), 56 * 1024, 0, m, c0); }},
-      V{"exact xcd lds56k", [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL((k_prod_xcd<false>), dim3(((n + 3) / 4 + 7) / 8 * 8), dim3(256), 56 * 1024, 0, m, c0); }},
-      LDSV("fast lds56k", (k_prod<true, 1>), 56 * 1024),
-      LDSV("fast w2", (k_prod_w2<true>), 0),
-      LDSV("fast w2 lds56k", (k_prod_w2<true>), 56 * 1024),
-      LDSV("exact w2 lds56k", (k_prod_w2<false>), 56 * 1024),
-      LDSV("exact lds56k", (k_prod<false, 1>), 56 * 1024),
-      LDSV("exact (159, occ3)", (k_prod<false, 1>), 0),
-      LDSV("fast lb3 (168, occ3)", (k_prod<true, 3>), 0),
-      LDSV("exact w3", (k_prod_w3<false>), 0),
-      LDSV("fast lb1 (170 vgpr) again", (k_prod<true, 1>), 0),
-      LDSV("exact lds56k again", (k_prod<false, 1>), 56 * 1024),
+#define XCDV(NAME, K, LDS) V{NAME, [](const MainArgs& m, int c0, int n) { hipLaunchKernelGGL(K, dim3(((n + 3) / 4 + 7) / 8 * 8), dim3(256), LDS, 0, m, c0); }}
+      XCDV("xcd fast occ2", (k_prod_xcd<true>), 56 * 1024),
+      XCDV("xcd fast occ3", (k_prod_xcd<true>), 40 * 1024),
+      XCDV("xcd exact occ3", (k_prod_xcd<false>), 40 * 1024),
+      XCDV("xcd exact occ2", (k_prod_xcd<false>), 56 * 1024),
+      XCDV("xcd fast occ1", (k_prod_xcd<true>), 100 * 1024),
+      XCDV("xcd fast occ2 again", (k_prod_xcd<true>), 56 * 1024),
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
