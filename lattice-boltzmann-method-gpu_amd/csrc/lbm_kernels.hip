@@ -79,8 +79,8 @@ template <int Q>
 __device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t cb, int64_t c,
                                            int pitch, int64_t plane) {
   const int64_t ro = row_off<Q>(pitch, plane);
-  // non-temporal: every slice is read once per step (-8% kernel time at 512^3 vs plain
-  // loads; the edge floats and the lines two chunks share still meet in the XCD's L2)
+  // non-temporal: every slice is read once per step (no measurable change against plain
+  // loads in interleaved A/B runs; the lines two chunks share still meet in the XCD's L2)
   a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + aidx(c - ro, Q)));
   if constexpr (Dir<Q>::x == 1) e = src[aidx(cb - ro - 1, Q)];                  // lane 0: b - 1
   else if constexpr (Dir<Q>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];       // lane 63: b + 4
