@@ -48,9 +48,39 @@ typedef enum {
                               2 moving lid (velocity NEE, -y face), 3 fluid */
   LBM_CASE_POISEUILLE = 1, /* Poiseulle.cu: -1 ghost, 0 unused, 1 wall, 2 inlet (velocity NEE,
                               +y face), 3 outlet (velocity NEE, -y face), 4 fluid */
-  LBM_CASE_MASK = 2        /* bifurcation.cu: as Poiseuille but 3 = pressure outlet (rho = 1,
+  LBM_CASE_MASK = 2,       /* bifurcation.cu: as Poiseuille but 3 = pressure outlet (rho = 1,
                               u = u of the fluid neighbour) */
+  LBM_CASE_GENERIC = 3     /* 4 fluid, 1 wall, boundary codes from lbm_desc.bc_codes (any face and
+                              kind, e.g. coronary.cu:716-944's +-x inlet/outlet and -z outlets);
+                              every other code is passive */
 } lbm_case_kind;
+
+/* Which side of a boundary cell its fluid neighbour lies on.  The boundary supplies the
+ * populations q with e_q pointing into the fluid (e_q . n = +1 along the face's axis):
+ * LDC lid at y = ny-2 over fluid at y = ny-3 -> LBM_FACE_NY (q = 4, 8, 10, 16, 18). */
+typedef enum { LBM_FACE_PX = 0, LBM_FACE_NX = 1, LBM_FACE_PY = 2, LBM_FACE_NY = 3, LBM_FACE_PZ = 4,
+               LBM_FACE_NZ = 5 } lbm_face;
+
+/* Non-equilibrium extrapolation: f_q(B) = feq_q(rho_bc, u_bc) + (f_q(F) - feq_q(rho_F, u_F)) (1 - 1/tau)
+ * with F the fluid neighbour and its previous-step macros. */
+typedef enum {
+  LBM_BC_VELOCITY = 0,      /* u_bc given, rho_bc = rho_F (LDC lid, Poiseuille, bifurcation inlet,
+                               coronary outlets coronary.cu:795-943) */
+  LBM_BC_VELOCITY_RHO = 1,  /* u_bc and rho_bc given (coronary inlet, rho_bc = 1, coronary.cu:716-794) */
+  LBM_BC_PRESSURE = 2       /* rho_bc given, u_bc = u_F (bifurcation outlet, bifurcation.cu:877-948) */
+} lbm_bc_kind;
+
+typedef struct {
+  int code;                 /* mask value of the boundary cells (2, 3, 5..127) */
+  int face;                 /* lbm_face */
+  int kind;                 /* lbm_bc_kind */
+  float rho;                /* rho_bc (LBM_BC_VELOCITY_RHO, LBM_BC_PRESSURE) */
+  float u[3];               /* u_bc (velocity kinds) */
+  /* Nullable per-cell profile replacing u[axis of face]: raster over the face's two other axes
+   * (x faces [nz_global][ny], y faces [nz_global][nx], z faces [ny][nx]; global z).  Copied at
+   * lbm_create. */
+  const float* u_normal_table;
+} lbm_bc_code;
 
 /* Equilibrium expression used to initialise f (the two forms of the reference). */
 typedef enum {
@@ -80,6 +110,9 @@ typedef struct {
    * row; 0 = choose it from geo so that most rows start their fluid run on a 4-cell boundary.
    * Slabs of one lattice must use the same value (lbm_attach_rccl / lbm_group_step check). */
   int x_align;
+  /* LBM_CASE_GENERIC: the boundary codes (at most 16; copied at lbm_create). */
+  const lbm_bc_code* bc_codes;
+  int n_bc_codes;
 } lbm_desc;
 
 /* Status / version */

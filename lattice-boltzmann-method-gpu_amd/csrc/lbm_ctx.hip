@@ -313,8 +313,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   }
   *out = nullptr;
   const lbm_desc& d = *desc;
-  if (d.nx < 3 || d.ny < 3 || d.nz < 1 || !(d.tau > 0.f) || d.case_kind < 0 || d.case_kind > 2 || d.x_align < 0 ||
-      d.x_align > 4) {
+  if (d.nx < 3 || d.ny < 3 || d.nz < 1 || !(d.tau > 0.f) || d.case_kind < 0 || d.case_kind > 3 || d.x_align < 0 ||
+      d.x_align > 4 || d.n_bc_codes < 0 || d.n_bc_codes > kMaxBcCodes || (d.n_bc_codes > 0 && !d.bc_codes)) {
     g_create_error = "invalid lattice description";
     return LBM_ERR_ARG;
   }
@@ -327,6 +327,16 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   c->d.geo = nullptr;
   c->d.bc_inlet_uy = nullptr;
   c->d.bc_outlet_uy = nullptr;
+  c->d.bc_codes = nullptr;
+  for (int k = 0; k < d.n_bc_codes; ++k) {
+    const lbm_bc_code& b = d.bc_codes[k];
+    if (b.face < 0 || b.face > 5 || b.kind < 0 || b.kind > 2 || b.code == 1 || b.code == 4 || b.code < -128 ||
+        b.code > 127) {
+      g_create_error = "invalid boundary code entry " + std::to_string(k);
+      delete c;
+      return LBM_ERR_ARG;
+    }
+  }
   if (c->d.nz_global <= 0) c->d.nz_global = d.nz;
   c->tau = d.tau;
   c->omc = 1.0f - 1.0f / d.tau;  // the reference's (1.0f - 1.0f / tau), evaluated in fp32
@@ -425,6 +435,26 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     CK(hipMemcpy(dout, desc->bc_outlet_uy, sizeof(float) * ntab, hipMemcpyHostToDevice));
   }
   GeoArgs g{};
+  std::vector<float*> bc_tables;
+  if (d.case_kind == LBM_CASE_GENERIC) {
+    g.nbc = d.n_bc_codes;
+    for (int k = 0; k < d.n_bc_codes; ++k) {
+      const lbm_bc_code& b = d.bc_codes[k];
+      BcCode& o = g.bcs[k];
+      o.code = b.code; o.face = b.face; o.kind = b.kind; o.rho = b.rho;
+      o.u[0] = b.u[0]; o.u[1] = b.u[1]; o.u[2] = b.u[2];
+      if (b.u_normal_table) {
+        const int axis = b.face >> 1;
+        const int64_t nt = axis == 0 ? (int64_t)d.ny * c->d.nz_global
+                                     : axis == 1 ? (int64_t)d.nx * c->d.nz_global : (int64_t)d.nx * d.ny;
+        float* t = nullptr;
+        CK(hipMalloc(&t, sizeof(float) * nt));
+        bc_tables.push_back(t);
+        CK(hipMemcpy(t, b.u_normal_table, sizeof(float) * nt, hipMemcpyHostToDevice));
+        o.table = t;
+      }
+    }
+  }
   g.codes = dcodes; g.type = c->type; g.links = c->links;
   g.rho = c->rho; g.ux = c->ux; g.uy = c->uy; g.uz = c->uz;
   g.inlet_uy = din; g.outlet_uy = dout;
@@ -437,6 +467,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   CK(hipFree(dcodes));
   if (din) CK(hipFree(din));
   if (dout) CK(hipFree(dout));
+  for (float* t : bc_tables) CK(hipFree(t));
 
   // ---- work lists: whole domain, and lo edge / hi edge / interior for slabs ----
   {

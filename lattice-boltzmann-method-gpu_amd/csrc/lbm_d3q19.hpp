@@ -145,6 +145,19 @@ template <> LBM_HD float feq<18>(float tmp_rho, float tmp_ux, float tmp_uy, floa
   return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_uy + tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
 }
 
+// Boundary-value equilibrium of the NEE boundaries.  The reference writes these as
+// hand-simplified fp32 "tmp" terms (ldc.cu:402-454, Poiseulle.cu:748-891,
+// bifurcation.cu:877-1021, coronary.cu:716-943): bit-identical to feq<Q> for every q they
+// use, except q = 14 on a z face (coronary.cu:870-871), where the tmp term keeps fp32 while
+// the update kernel's feq[14] has its fp64 sub-expression.
+template <int Q>
+LBM_HD float feq_bc(float r, float ux, float uy, float uz) {
+  return feq<Q>(r, ux, uy, uz);
+}
+template <> LBM_HD float feq_bc<14>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
+  return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz -1.5f* tmp_uy*tmp_uy);
+}
+
 // The LDC initialize() form (ldc.cu:542-571): all 19 at once.
 LBM_HD void feq_init_wi(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz, float* feq) {
   const float w0 = 1.0f / 3.0f, w1 = 1.0f / 18.0f, w2 = 1.0f / 36.0f;

@@ -315,12 +315,13 @@ __device__ __forceinline__ void fix_pull(float* f, const MainArgs& a, int64_t c,
       if (tn & kKindPressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
         rb = a.rho[nb];
         bx = mp.ux; by = mp.uy; bz = mp.uz;
-      } else {                   // u_bc stored at B; rho_bc = rho of the fluid neighbour
-        rb = mp.rho;
+      } else {                   // u_bc stored at B; rho_bc stored too, or NaN: that of the fluid cell
+        rb = a.rho[nb];
+        if (__builtin_isnan(rb)) rb = mp.rho;
         bx = a.ux[nb]; by = a.uy[nb]; bz = a.uz[nb];
       }
       const float own = a.src[aidx(c, Q)];
-      const float e_bc = feq<Q>(rb, bx, by, bz);
+      const float e_bc = feq_bc<Q>(rb, bx, by, bz);
       const float e_nb = feq<Q>(mp.rho, mp.ux, mp.uy, mp.uz);
       f[Q] = e_bc + (own - e_nb) * a.omc;
     }
@@ -551,13 +552,35 @@ __global__ void k_classify(const GeoArgs g) {
     const int zs = (int)(u / g.plane);
     const int zg = zs - 1 + g.z_offset;  // global z
     uint8_t t = kPassive;
+    const float kRhoOfFluid = __builtin_nanf("");  // rho slot of a velocity NEE cell: use rho_F
     if (x < g.nx && zs < g.planes) {
+      const int y = (int)((u / g.pitch) % g.ny);
       if (g.case_kind == 0) {  // LDC (ldc.cu:469): 0 ghost, 1 wall, 2 lid, 3 fluid
         if (code == 1) t = kWall;
         else if (code == 3) t = kFluid;
         else if (code == 2) {  // lid supplies {4,8,10,16,18} (ldc.cu:391-456), u = (0, 0, u_lid)
           t = make_nee(kFaceNY, false);
-          g.rho[c] = 0.f; g.ux[c] = 0.f; g.uy[c] = 0.f; g.uz[c] = g.lid_u;
+          g.rho[c] = kRhoOfFluid; g.ux[c] = 0.f; g.uy[c] = 0.f; g.uz[c] = g.lid_u;
+        }
+      } else if (g.case_kind == 3) {  // generic: 4 fluid, 1 wall, boundary codes by table
+        if (code == 4) t = kFluid;
+        else if (code == 1) t = kWall;
+        else {
+          for (int k = 0; k < g.nbc; ++k) {
+            const BcCode& b = g.bcs[k];
+            if (b.code != code) continue;
+            t = make_nee(b.face, b.kind == 2);
+            float v[3] = {b.u[0], b.u[1], b.u[2]};
+            const int axis = b.face >> 1;
+            if (b.table && zg >= 0 && zg < g.nz_global) {
+              const int64_t ti = axis == 0 ? y + (int64_t)zg * g.ny : axis == 1 ? x + (int64_t)zg * g.nx
+                                                                                 : x + (int64_t)y * g.nx;
+              v[axis] = b.table[ti];
+            }
+            g.rho[c] = b.kind == 0 ? kRhoOfFluid : b.rho;
+            g.ux[c] = v[0]; g.uy[c] = v[1]; g.uz[c] = v[2];
+            break;
+          }
         }
       } else {  // Poiseuille / mask (README.md:9-14)
         const bool in_tab = zg >= 0 && zg < g.nz_global;
@@ -565,13 +588,13 @@ __global__ void k_classify(const GeoArgs g) {
         else if (code == 4) t = kFluid;
         else if (code == 2) {   // inlet: +y face {3,7,9,15,17}, u = (0, inlet_uy(x,z), 0)
           t = make_nee(kFacePY, false);
-          const float u = (g.inlet_uy && in_tab) ? g.inlet_uy[x + (int64_t)zg * g.nx] : 0.f;
-          g.rho[c] = 0.f; g.ux[c] = 0.f; g.uy[c] = u; g.uz[c] = 0.f;
+          const float v = (g.inlet_uy && in_tab) ? g.inlet_uy[x + (int64_t)zg * g.nx] : 0.f;
+          g.rho[c] = kRhoOfFluid; g.ux[c] = 0.f; g.uy[c] = v; g.uz[c] = 0.f;
         } else if (code == 3) { // outlet: -y face {4,8,10,16,18}
           if (g.case_kind == 1) {  // Poiseuille: velocity, u = (0, outlet_uy(x,z), 0)
             t = make_nee(kFaceNY, false);
-            const float u = (g.outlet_uy && in_tab) ? g.outlet_uy[x + (int64_t)zg * g.nx] : 0.f;
-            g.rho[c] = 0.f; g.ux[c] = 0.f; g.uy[c] = u; g.uz[c] = 0.f;
+            const float v = (g.outlet_uy && in_tab) ? g.outlet_uy[x + (int64_t)zg * g.nx] : 0.f;
+            g.rho[c] = kRhoOfFluid; g.ux[c] = 0.f; g.uy[c] = v; g.uz[c] = 0.f;
           } else {                 // bifurcation: pressure, rho = 1 (bifurcation.cu:890)
             t = make_nee(kFaceNY, true);
             g.rho[c] = 1.0f; g.ux[c] = 0.f; g.uy[c] = 0.f; g.uz[c] = 0.f;

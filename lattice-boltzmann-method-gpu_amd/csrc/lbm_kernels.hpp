@@ -123,6 +123,14 @@ hipError_t launch_unpack(float* f, const float* buf, const uint8_t* type, int zs
 hipError_t launch_bb_prime(float* f, const uint8_t* type, const uint32_t* links, int64_t ncell, int pitch,
                            int64_t plane, hipStream_t s);
 
+// LBM_CASE_GENERIC boundary code on the device (lbm_bc_code with a device table)
+struct BcCode {
+  int code, face, kind;     // kind: 0 velocity (rho_bc = rho_F), 1 velocity + rho, 2 pressure
+  float rho, u[3];
+  const float* table;       // nullable: u along the face axis per cell (see lbm.h)
+};
+constexpr int kMaxBcCodes = 16;
+
 // geometry: reference codes (int8 per linear cell) -> cell-type bytes
 struct GeoArgs {
   const int8_t* codes;
@@ -136,6 +144,8 @@ struct GeoArgs {
   int nx, ny, pitch, xshift, planes;
   int64_t plane, ncell;
   int z_offset, nz_global;
+  BcCode bcs[kMaxBcCodes];  // LBM_CASE_GENERIC
+  int nbc;
 };
 hipError_t launch_classify(const GeoArgs& g, hipStream_t s);
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s);

@@ -27,7 +27,9 @@ LIB = os.path.join(ROOT, "lib")
 LIBLBM = os.environ.get("LBM_LIBRARY") or os.path.join(LIB, "liblbm.so")  # override: A/B builds
 LIBHOST = os.path.join(LIB, "liblbm_host.so")
 
-LBM_CASE_LDC, LBM_CASE_POISEUILLE, LBM_CASE_MASK = 0, 1, 2
+LBM_CASE_LDC, LBM_CASE_POISEUILLE, LBM_CASE_MASK, LBM_CASE_GENERIC = 0, 1, 2, 3
+LBM_FACE_PX, LBM_FACE_NX, LBM_FACE_PY, LBM_FACE_NY, LBM_FACE_PZ, LBM_FACE_NZ = range(6)
+LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_BC_PRESSURE = 0, 1, 2
 LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
 
 # reference per-case constants
@@ -46,6 +48,14 @@ class LbmError(RuntimeError):
     pass
 
 
+class lbm_bc_code(C.Structure):
+    _fields_ = [
+        ("code", C.c_int), ("face", C.c_int), ("kind", C.c_int),
+        ("rho", C.c_float), ("u", C.c_float * 3),
+        ("u_normal_table", C.POINTER(C.c_float)),
+    ]
+
+
 class lbm_desc(C.Structure):
     _fields_ = [
         ("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int),
@@ -60,6 +70,8 @@ class lbm_desc(C.Structure):
         ("z_offset", C.c_int),
         ("nz_global", C.c_int),
         ("x_align", C.c_int),
+        ("bc_codes", C.POINTER(lbm_bc_code)),
+        ("n_bc_codes", C.c_int),
     ]
 
 
@@ -266,7 +278,8 @@ class Lattice:
 
     def __init__(self, case_kind: int, shape, tau: float, geo: np.ndarray | None = None, *,
                  halo_planes: bool = False, lid_u_val: float | None = None, inlet_uy=None, outlet_uy=None,
-                 device: int = 0, z_offset: int = 0, nz_global: int | None = None, x_align: int = 0):
+                 device: int = 0, z_offset: int = 0, nz_global: int | None = None, x_align: int = 0,
+                 bc_codes=None):
         nz, ny, nx = shape
         self.shape = (nz, ny, nx)
         self.case_kind = case_kind
@@ -293,6 +306,20 @@ class Lattice:
         d.z_offset = z_offset
         d.nz_global = nz if nz_global is None else nz_global
         d.x_align = x_align
+        if bc_codes:
+            arr = (lbm_bc_code * len(bc_codes))()
+            for k, b in enumerate(bc_codes):
+                arr[k].code, arr[k].face, arr[k].kind = b["code"], b["face"], b["kind"]
+                arr[k].rho = b.get("rho", 1.0)
+                for i, v in enumerate(b.get("u", (0.0, 0.0, 0.0))):
+                    arr[k].u[i] = v
+                if b.get("table") is not None:
+                    t = np.ascontiguousarray(b["table"], np.float32)
+                    self._keep.append(t)
+                    arr[k].u_normal_table = _ptr(t, C.c_float)
+            self._keep.append(arr)
+            d.bc_codes = C.cast(arr, C.POINTER(lbm_bc_code))
+            d.n_bc_codes = len(bc_codes)
         self.desc = d
         h = P()
         rc = lbm_lib().lbm_create(C.byref(d), C.byref(h))

@@ -59,6 +59,52 @@ def bifurcation(inlet_block: int = 0, geo_path: str | None = None, bc_path: str 
     return lat, geo, inl, outl
 
 
+def duct_generic(nx: int, ny: int, nz: int, u_in: float = 0.05, u_out: float = 0.045, u_side: float = 0.01):
+    """A coronary-style test geometry for LBM_CASE_GENERIC (coronary.cu:716-944's boundary
+    scheme on every kind of face): a duct along x with
+      code 2  inlet at x = 1, face +x, velocity + rho = 1 (parabolic u_x table over y,z),
+      code 3  outlet at x = nx-2, face -x, velocity with rho of the fluid,
+      code 5  side outlet patch in the top wall z = nz-2, face -z, velocity (0, 0, u_side),
+      code 6  pressure patch in the y = 1 wall, face +y, rho = 1, u of the fluid.
+    Returns (geo [nz][ny][nx] int8, bc_codes list of dicts, initial (rho, ux, uy, uz))."""
+    g = np.zeros((nz, ny, nx), np.int8)
+    g[1:nz - 1, 1:ny - 1, 1:nx - 1] = 1
+    g[2:nz - 2, 2:ny - 2, 2:nx - 2] = 4
+    g[2:nz - 2, 2:ny - 2, 1] = 2
+    g[2:nz - 2, 2:ny - 2, nx - 2] = 3
+    cx, cy = nx // 2, ny // 2
+    g[nz - 2, cy - 2:cy + 3, cx - 2:cx + 3] = 5
+    g[3:6, 1, 4:7] = 6
+    yy, zz = np.meshgrid(np.arange(ny, dtype=np.float32), np.arange(nz, dtype=np.float32))
+    ry, rz = np.float32((ny - 5) / 2.0), np.float32((nz - 5) / 2.0)
+    prof = np.float32(u_in) * (np.float32(1) - ((yy - np.float32((ny - 1) / 2)) / ry) ** 2) * \
+        (np.float32(1) - ((zz - np.float32((nz - 1) / 2)) / rz) ** 2)
+    prof = np.clip(prof, 0, None).astype(np.float32)  # [z][y]
+    bcs = [
+        {"code": 2, "face": 0, "kind": 1, "rho": 1.0, "u": (u_in, 0.0, 0.0), "table": prof},
+        {"code": 3, "face": 1, "kind": 0, "u": (u_out, 0.0, 0.0)},
+        {"code": 5, "face": 5, "kind": 0, "u": (0.0, 0.0, u_side)},
+        {"code": 6, "face": 2, "kind": 2, "rho": 1.0},
+    ]
+    rho = np.where(g != 0, np.float32(1), np.float32(1)).astype(np.float32)
+    ux = np.zeros(g.shape, np.float32)
+    uy = np.zeros(g.shape, np.float32)
+    uz = np.zeros(g.shape, np.float32)
+    ux[g == 2] = prof[g[:, :, 1] == 2]
+    ux[g == 3] = np.float32(u_out)
+    uz[g == 5] = np.float32(u_side)
+    return g, bcs, (rho, ux, uy, uz)
+
+
+def generic(geo, bcs, fields, tau: float = 0.6, device: int = 0):
+    """A LBM_CASE_GENERIC lattice initialised at the equilibrium of `fields` (expanded form)."""
+    from . import LBM_CASE_GENERIC
+    nz, ny, nx = geo.shape
+    lat = Lattice(LBM_CASE_GENERIC, (nz, ny, nx), tau, geo, device=device, bc_codes=bcs)
+    lat.init_equilibrium(LBM_INIT_EXPANDED, *fields)
+    return lat
+
+
 def slab_bounds(nz_global: int, nslabs: int, i: int):
     """z range [z0, z1) of slab i of an even split (remainder to the lowest slabs)."""
     base, rem = divmod(nz_global, nslabs)

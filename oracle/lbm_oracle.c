@@ -31,6 +31,8 @@ struct orc_lbm {
     float *inlet_uy, *outlet_uy;     /* nx*nz tables (POISEUILLE: kernel uygt; MASK: bc.txt) */
     long bad_reads;
     int steps;
+    orc_bc bcs[16];                  /* ORC_GENERIC (tables owned) */
+    int nbc;
     float sum_current;               /* ldc.cu:652 sum_current */
 };
 
@@ -245,6 +247,14 @@ static void feq_update(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz, 
     feq[18] = tmp_rho /36.0f * (1.0f - 3.0f* (tmp_uy + tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
 }
 
+/* boundary-value equilibrium: the reference's NEE "tmp" terms are fp32 throughout; they equal
+ * feq_update for every q they use except q = 14 on a z face (coronary.cu:870-871), where the
+ * fp64 sub-expression of the update form is absent */
+static void feq_bc(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz, float* feq) {
+    feq_update(tmp_rho, tmp_ux, tmp_uy, tmp_uz, feq);
+    feq[14] = tmp_rho /36.0f * (1.0f - 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz -1.5f* tmp_uy*tmp_uy);
+}
+
 /* the LDC initialize() form, ldc.cu:542-571 */
 static void feq_init_ldc(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz, float* feq) {
     static const float wi[19] = { 1.0f / 3.0f, 1.0f / 18.0f,1.0f / 18.0f,1.0f / 18.0f,1.0f / 18.0f,1.0f / 18.0f,1.0f / 18.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f,1.0f / 36.0f };
@@ -307,8 +317,68 @@ orc_lbm* orc_create(int kind, int nx, int ny, int nz, const int8_t* geo, float t
     return o;
 }
 
+orc_lbm* orc_create_generic(int nx, int ny, int nz, const int8_t* geo, float tau, const orc_bc* bcs, int nbc) {
+    if (nbc < 0 || nbc > 16) return NULL;
+    orc_lbm* o = orc_create(ORC_GENERIC, nx, ny, nz, geo, tau, ORC_LDC_TWO_PHASE, NULL, NULL);
+    o->nbc = nbc;
+    for (int k = 0; k < nbc; k++) {
+        o->bcs[k] = bcs[k];
+        if (bcs[k].table) {
+            int axis = bcs[k].face >> 1;
+            long nt = axis == 0 ? (long)ny * nz : axis == 1 ? (long)nx * nz : (long)nx * ny;
+            float* t = (float*)malloc(sizeof(float) * (size_t)nt);
+            memcpy(t, bcs[k].table, sizeof(float) * (size_t)nt);
+            o->bcs[k].table = t;
+        }
+    }
+    return o;
+}
+
+void orc_feq(float rho, float ux, float uy, float uz, float* feq19) { feq_update(rho, ux, uy, uz, feq19); }
+void orc_feq_bc(float rho, float ux, float uy, float uz, float* feq19) { feq_bc(rho, ux, uy, uz, feq19); }
+
+/* the boundary velocity of code entry b at cell (x,y,z) */
+static void bc_velocity(const orc_lbm* o, const orc_bc* b, int x, int y, int z, float* u) {
+    u[0] = b->u[0]; u[1] = b->u[1]; u[2] = b->u[2];
+    if (b->table) {
+        int axis = b->face >> 1;
+        long ti = axis == 0 ? y + (long)z * o->ny : axis == 1 ? x + (long)z * o->nx : x + (long)y * o->nx;
+        u[axis] = b->table[ti];
+    }
+}
+
+static const orc_bc* find_bc(const orc_lbm* o, int code) {
+    for (int k = 0; k < o->nbc; k++)
+        if (o->bcs[k].code == code) return &o->bcs[k];
+    return NULL;
+}
+
+/* generic NEE cell (coronary.cu:716-944 generalised) */
+static void nee_generic_cell(orc_lbm* o, const orc_bc* b, int x, int y, int z) {
+    const long n = o->ncell;
+    const long c = cidx(o, x, y, z);
+    const float tau = o->tau;
+    const int axis = b->face >> 1, sgn = (b->face & 1) ? -1 : 1;
+    float ubc[3];
+    bc_velocity(o, b, x, y, z, ubc);
+    for (int q = 1; q < 19; q++) {
+        int e = axis == 0 ? EX[q] : axis == 1 ? EY[q] : EZ[q];
+        if (e != sgn) continue;
+        int x2 = x + EX[q], y2 = y + EY[q], z2 = z + EZ[q];
+        if (x2 < 0 || y2 < 0 || z2 < 0 || x2 >= o->nx || y2 >= o->ny || z2 >= o->nz) continue;
+        long c2 = cidx(o, x2, y2, z2);
+        float tmp_rho = o->rho[c2], tmp_ux = o->ux[c2], tmp_uy = o->uy[c2], tmp_uz = o->uz[c2];
+        float feq[19], ebc[19];
+        feq_update(tmp_rho, tmp_ux, tmp_uy, tmp_uz, feq);
+        if (b->kind == 2) feq_bc(b->rho, tmp_ux, tmp_uy, tmp_uz, ebc);
+        else feq_bc(b->kind == 1 ? b->rho : tmp_rho, ubc[0], ubc[1], ubc[2], ebc);
+        o->dst[q * n + c] = ebc[q] + (o->dst[q * n + c2] - feq[q])*(1.0f - 1.0f / tau);
+    }
+}
+
 void orc_destroy(orc_lbm* o) {
     if (!o) return;
+    for (int k = 0; k < o->nbc; k++) free((void*)o->bcs[k].table);
     free(o->geo); free(o->src); free(o->dst);
     free(o->rho); free(o->ux); free(o->uy); free(o->uz);
     free(o->inlet_uy); free(o->outlet_uy);
@@ -329,6 +399,19 @@ void orc_initialize(orc_lbm* o) {
                     long c = cidx(o, x, y, z);
                     float uz = (y == ny - 1 || y == ny - 2) ? u_max : 0.0f;
                     feq_init_ldc(1.0f, 0.0f, 0.0f, uz, feq);
+                    for (int q = 0; q < 19; q++) o->src[q * n + c] = o->dst[q * n + c] = feq[q];
+                }
+    } else if (o->kind == ORC_GENERIC) {
+        /* coronary.cu:280-330 generalised: stored cells at rest, velocity-boundary cells at u_bc */
+        for (int z = 0; z < nz; z++)
+            for (int y = 0; y < ny; y++)
+                for (int x = 0; x < nx; x++) {
+                    long c = cidx(o, x, y, z);
+                    if (o->geo[c] == 0) continue;
+                    float u[3] = {0.0f, 0.0f, 0.0f};
+                    const orc_bc* b = find_bc(o, o->geo[c]);
+                    if (b && b->kind != 2) bc_velocity(o, b, x, y, z, u);
+                    feq_update(1.0f, u[0], u[1], u[2], feq);
                     for (int q = 0; q < 19; q++) o->src[q * n + c] = o->dst[q * n + c] = feq[q];
                 }
     } else {
@@ -548,6 +631,18 @@ static void step_once(orc_lbm* o) {
             for (int y = 0; y < ny; y++)
                 for (int x = 0; x < nx; x++)
                     if (o->geo[cidx(o, x, y, z)] == 2) ldc_lid_cell(o, x, y, z);
+    } else if (o->kind == ORC_GENERIC) {
+        update_pass(o, 4);
+        for (int z = 0; z < nz; z++)
+            for (int y = 0; y < ny; y++)
+                for (int x = 0; x < nx; x++)
+                    if (o->geo[cidx(o, x, y, z)] == 1) post_wall_cell(o, x, y, z);
+        for (int z = 0; z < nz; z++)
+            for (int y = 0; y < ny; y++)
+                for (int x = 0; x < nx; x++) {
+                    const orc_bc* b = find_bc(o, o->geo[cidx(o, x, y, z)]);
+                    if (b) nee_generic_cell(o, b, x, y, z);
+                }
     } else {
         update_pass(o, fc);
         for (int z = 0; z < nz; z++)

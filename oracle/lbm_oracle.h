@@ -37,7 +37,19 @@
 extern "C" {
 #endif
 
-enum { ORC_LDC = 0, ORC_POISEUILLE = 1, ORC_MASK = 2 };
+enum { ORC_LDC = 0, ORC_POISEUILLE = 1, ORC_MASK = 2, ORC_GENERIC = 3 };
+
+/* Generic non-equilibrium-extrapolation boundary code (the coronary case's scheme,
+ * coronary.cu:716-944, generalised to any face): for a cell with this code and every q with
+ * e_q pointing to the fluid side (face: 0 +x, 1 -x, 2 +y, 3 -y, 4 +z, 5 -z),
+ *   f_q(B) = feq_q(rho_bc, u_bc) + (f_q(B + e_q) - feq_q(rho_nb, u_nb)) (1 - 1/tau)
+ * kind 0: u_bc = u, rho_bc = rho_nb;  1: u_bc = u, rho_bc = rho;  2: rho_bc = rho, u_bc = u_nb.
+ * table (nullable) replaces u[face axis] per cell: x faces [z][y], y faces [z][x], z faces [y][x]. */
+typedef struct {
+    int code, face, kind;
+    float rho, u[3];
+    const float* table;
+} orc_bc;
 /* LDC wall bounce-back ordering: the reference (ldc.cu:184-201 vs 204-313) races. */
 enum { ORC_LDC_TWO_PHASE = 0,   /* all wall writes before any fluid read (race-free) */
        ORC_LDC_SERIAL_EMU = 1 }; /* serial emulation order: blocks z,y,x; threads y,x; koff 7..0 */
@@ -59,7 +71,14 @@ int  orc_index_transform(int nx, int ny, int nz, const int8_t* geo, int32_t* ind
 /* ---- solver ---- */
 orc_lbm* orc_create(int case_kind, int nx, int ny, int nz, const int8_t* geo, float tau,
                     int ldc_order, const float* inlet_uy, const float* outlet_uy);
+/* ORC_GENERIC: 4 fluid, 1 wall (post-collision bounce-back as Poiseulle.cu:601-746), the
+ * listed boundary codes (at most 16), everything else unstored. */
+orc_lbm* orc_create_generic(int nx, int ny, int nz, const int8_t* geo, float tau, const orc_bc* bcs, int nbc);
 void orc_destroy(orc_lbm* o);
+/* the update kernel's equilibrium (Poiseulle.cu:561-580 expression trees) */
+void orc_feq(float rho, float ux, float uy, float uz, float* feq19);
+/* the boundary-value equilibrium of the NEE "tmp" terms (fp32 throughout) */
+void orc_feq_bc(float rho, float ux, float uy, float uz, float* feq19);
 /* reference initialize(): LDC wi-form (ldc.cu:504-580) / expanded form (Poiseulle.cu:273-382,
  * bifurcation.cu:329-427), with each case's initial rho/u rules. */
 void orc_initialize(orc_lbm* o);

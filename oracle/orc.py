@@ -14,7 +14,12 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblbm_oracle.so")
 
-LDC, POISEUILLE, MASK = 0, 1, 2
+LDC, POISEUILLE, MASK, GENERIC = 0, 1, 2, 3
+
+
+class orc_bc(C.Structure):
+    _fields_ = [("code", C.c_int), ("face", C.c_int), ("kind", C.c_int), ("rho", C.c_float),
+                ("u", C.c_float * 3), ("table", C.POINTER(C.c_float))]
 TWO_PHASE, SERIAL_EMU = 0, 1
 
 _lib = None
@@ -44,6 +49,9 @@ def lib() -> C.CDLL:
             "orc_index_transform": (C.c_int, [C.c_int, C.c_int, C.c_int, i8p, i32p]),
             "orc_create": (P, [C.c_int, C.c_int, C.c_int, C.c_int, i8p, C.c_float, C.c_int, f32p, f32p]),
             "orc_destroy": (None, [P]),
+            "orc_create_generic": (P, [C.c_int, C.c_int, C.c_int, i8p, C.c_float, C.POINTER(orc_bc), C.c_int]),
+            "orc_feq": (None, [C.c_float, C.c_float, C.c_float, C.c_float, f32p]),
+            "orc_feq_bc": (None, [C.c_float, C.c_float, C.c_float, C.c_float, f32p]),
             "orc_initialize": (None, [P]),
             "orc_step": (None, [P, C.c_int, f32p]),
             "orc_run_converge": (C.c_int, [P, C.c_int, C.c_int, C.c_float, f32p]),
@@ -115,7 +123,7 @@ class Oracle:
     """Serial CPU restatement of one reference case."""
 
     def __init__(self, kind: int, geo: np.ndarray, tau: float, ldc_order: int = TWO_PHASE,
-                 inlet_uy: np.ndarray | None = None, outlet_uy: np.ndarray | None = None):
+                 inlet_uy: np.ndarray | None = None, outlet_uy: np.ndarray | None = None, bcs=None):
         self.geo = np.ascontiguousarray(geo, np.int8)
         self.nz, self.ny, self.nx = self.geo.shape
         self.kind = kind
@@ -125,14 +133,28 @@ class Oracle:
             a = np.ascontiguousarray(inlet_uy, np.float32); self._keep.append(a); ip = _p(a, C.c_float)
         if outlet_uy is not None:
             a = np.ascontiguousarray(outlet_uy, np.float32); self._keep.append(a); op = _p(a, C.c_float)
-        self.h = lib().orc_create(kind, self.nx, self.ny, self.nz, _p(self.geo, C.c_int8), float(tau),
-                                  ldc_order, ip, op)
+        if kind == GENERIC:
+            arr = (orc_bc * max(1, len(bcs or [])))()
+            for k, b in enumerate(bcs or []):
+                arr[k].code, arr[k].face, arr[k].kind = b["code"], b["face"], b["kind"]
+                arr[k].rho = b.get("rho", 1.0)
+                for i, v in enumerate(b.get("u", (0.0, 0.0, 0.0))):
+                    arr[k].u[i] = v
+                if b.get("table") is not None:
+                    t = np.ascontiguousarray(b["table"], np.float32)
+                    self._keep.append(t)
+                    arr[k].table = _p(t, C.c_float)
+            self.h = lib().orc_create_generic(self.nx, self.ny, self.nz, _p(self.geo, C.c_int8), float(tau), arr,
+                                              len(bcs or []))
+        else:
+            self.h = lib().orc_create(kind, self.nx, self.ny, self.nz, _p(self.geo, C.c_int8), float(tau),
+                                      ldc_order, ip, op)
         lib().orc_initialize(self.h)
 
     def __del__(self):
         h = getattr(self, "h", None)
-        if h:
-            lib().orc_destroy(h)
+        if h and _lib is not None:
+            _lib.orc_destroy(h)
             self.h = None
 
     @property
@@ -172,6 +194,20 @@ class Oracle:
 
     def velsum(self) -> float:
         return float(lib().orc_velsum(self.h))
+
+
+def feq(rho: float, ux: float, uy: float, uz: float) -> np.ndarray:
+    """The update kernel's equilibrium (Poiseulle.cu:561-580) in fp32."""
+    out = np.zeros(19, np.float32)
+    lib().orc_feq(rho, ux, uy, uz, _p(out, C.c_float))
+    return out
+
+
+def feq_bc(rho: float, ux: float, uy: float, uz: float) -> np.ndarray:
+    """The NEE boundary-value equilibrium (the reference's fp32 tmp terms)."""
+    out = np.zeros(19, np.float32)
+    lib().orc_feq_bc(rho, ux, uy, uz, _p(out, C.c_float))
+    return out
 
 
 # reference per-case constants (ldc.cu:48-55, Poiseulle.cu:38-44, bifurcation.cu:19-20,434)

@@ -47,13 +47,15 @@ def test_python_mirror_binds_every_symbol(lbm):
         assert getattr(H, name).argtypes is not None, name
 
 
-def test_desc_layout_matches_header(lbm):
-    """lbm_desc field order in the ctypes mirror follows include/lbm.h."""
+@pytest.mark.parametrize("name", ["lbm_desc", "lbm_bc_code"])
+def test_struct_layout_matches_header(lbm, name):
+    """Field order of the ctypes mirrors follows include/lbm.h."""
     text = open(os.path.join(REPO, "include", "lbm.h")).read()
-    body = text[text.index("typedef struct {"):text.index("} lbm_desc;")]
+    end = text.index("} " + name + ";")
+    body = text[text.rindex("typedef struct {", 0, end):end]
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    fields = re.findall(r"\b([a-z_][a-z0-9_]*)\s*(?:,|;)", body)
-    assert [f[0] for f in lbm.lbm_desc._fields_] == fields
+    fields = re.findall(r"\b([a-z_][a-z0-9_]*)\s*(?:\[\d+\])?\s*(?:,|;)", body)
+    assert [f[0] for f in getattr(lbm, name)._fields_] == fields
 
 
 def test_loads_without_device_and_fails_loudly(lbm):

@@ -103,3 +103,34 @@ def test_poiseuille_converge_pin(oracle):
     assert k == 6230
     uy = o.macros()[2]
     assert abs(float(uy[g == 4].max()) - 0.096993) < 5e-7
+
+
+def test_generic_nee_matches_coronary_expressions(oracle):
+    """coronary.cu writes its boundary equilibria as hand-simplified 'tmp' expressions
+    (inlet 716-794 with rho 1, outlets 795-943 with rho of the fluid); the generic oracle (and
+    liblbm) use feq_bc: the update kernel's feq_q in fp32 throughout.  Same bits for every u
+    tried -- and the update form itself differs at q = 14 on a z face (its fp64 term)."""
+    rng = np.random.default_rng(1)
+    f32 = np.float32
+    for u in np.concatenate([rng.uniform(-0.2, 0.2, 400), [0.1745 / 1.5441, 0.1 / 1.5441, 0.02 / 1.5441]]):
+        u = f32(u)
+        rho = f32(rng.uniform(0.9, 1.1))
+        one = f32(1.0)
+        # inlet, face +x, rho_bc = 1, u_bc = (u, 0, 0): q = 1 (w 1/18), 7, 8, 11, 12 (w 1/36)
+        e = oracle.feq_bc(1.0, float(u), 0.0, 0.0)
+        assert e[1] == one / f32(18) * (one + f32(3) * u + f32(3) * u * u)
+        for q in (7, 8, 11, 12):
+            assert e[q] == one / f32(36) * (one + f32(3) * u + f32(3) * u * u)
+        # outlet, face -x, rho_bc = rho_F: q = 2, 9, 10, 13, 14
+        e = oracle.feq_bc(float(rho), float(u), 0.0, 0.0)
+        assert e[2] == rho / f32(18) * (one - f32(3) * u + f32(3) * u * u)
+        for q in (9, 10, 13, 14):
+            assert e[q] == rho / f32(36) * (one - f32(3) * u + f32(3) * u * u)
+        # z outlets, face -z, u_bc = (0, 0, u): q = 6, 12, 14, 17, 18
+        e = oracle.feq_bc(float(rho), 0.0, 0.0, float(u))
+        assert e[6] == rho / f32(18) * (one - f32(3) * u + f32(3) * u * u)
+        for q in (12, 14, 17, 18):
+            assert e[q] == rho / f32(36) * (one - f32(3) * u + f32(3) * u * u)
+    e_upd = oracle.feq(1.05, 0.0, 0.0, 0.0123)
+    e_bc = oracle.feq_bc(1.05, 0.0, 0.0, 0.0123)
+    assert np.array_equal(np.delete(e_upd, 14), np.delete(e_bc, 14))
