@@ -312,3 +312,38 @@ def test_generic_boundaries_bitwise(gpu, oracle, shape):
         assert_bitwise(lat, o, geo, 2, f"generic {shape} +{s}")
         assert_residuals(hg, ho)
     assert o.bad_reads() == 0
+
+
+@pytest.mark.parametrize("shape", [(37, 29, 23), (13, 11, 7), (66, 9, 31)])
+def test_ragged_shapes_bitwise(gpu, oracle, shape):
+    """Extents that are not multiples of 4 (row padding, row shift, chunks straddling rows
+    and planes) and very flat boxes."""
+    from lbm_amd import cases
+    nx, ny, nz = shape
+    lat, geo = cases.ldc(nx, ny, nz)
+    o = oracle.Oracle(oracle.LDC, geo, 0.55)
+    lat.step(17, history=False)
+    o.step(17)
+    assert_bitwise(lat, o, geo, 0, f"ldc {shape}")
+    lat, geo = cases.poiseuille(nx, ny, nz)
+    o = oracle.Oracle(oracle.POISEUILLE, geo, 0.58)
+    lat.step(17, history=False)
+    o.step(17)
+    assert_bitwise(lat, o, geo, 1, f"poiseuille {shape}")
+
+
+def test_thin_slabs_loopback(gpu):
+    """Slabs of one and two planes (edge ranges overlapping / covering the whole slab)."""
+    from lbm_amd import cases
+    import lbm_amd
+    nz = 7
+    one = cases.ldc_device(20, 18, nz)
+    bounds = [(0, 1), (1, 3), (3, 4), (4, 7)]
+    slabs = [(z0, z1, cases.ldc_device(20, 18, z1 - z0, z_offset=z0, nz_global=nz)) for z0, z1 in bounds]
+    h1 = one.step(25)
+    hs = lbm_amd.group_step([s[2] for s in slabs], 25)
+    np.testing.assert_allclose(hs, h1, rtol=0, atol=1e-6)
+    ref = one.macros()
+    for z0, z1, lat in slabs:
+        for a, b in zip(lat.macros(), ref):
+            assert np.array_equal(a.view(np.uint32), b[z0:z1].view(np.uint32))
