@@ -45,6 +45,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int* retry = nullptr;   // fast-quotient domain misses: queued chunk ids (capacity nchunks)
   int* retry_cnt = nullptr;  // their count (emptied by the reduction launch)
   int main_blocks = 0, nee_blocks = 0;
+  bool quarter = false;   // one cell per lane (small ranges)
 };
 }  // namespace
 
@@ -192,12 +193,12 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, b
   a.type = c->type; a.links = c->links;
   a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
   a.partial = r.part;
-  a.chunks = r.chunks; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks;
+  a.chunks = r.chunks; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.tau = c->tau;
   a.tau_rcp = 1.0f / c->tau;
-  a.fast_div = (c->fast_div && allow_fast && r.retry) ? 1 : 0;
+  a.fast_div = (c->fast_div && allow_fast && r.retry && !r.quarter) ? 1 : 0;
   a.retry = r.retry;
   a.retry_count = a.fast_div ? r.retry_cnt : nullptr;
   a.store_all_macros = store_all ? 1 : 0;
@@ -248,7 +249,11 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMalloc(&r.prev, sizeof(float4) * r.nslow));
     HIPCK(c, hipMemset(r.prev, 0, sizeof(float4) * r.nslow));
   }
-  r.main_blocks = main_grid(r.nchunks);
+  {
+    const char* e = std::getenv("LBM_CELLS_PER_LANE");  // A/B switch: 1 or 4 (default: by size)
+    r.quarter = e ? (e[0] == '1') : (r.nchunks <= kQuarterMaxChunks);
+  }
+  r.main_blocks = main_grid(r.nchunks, r.quarter);
   r.nee_blocks = nee_grid(r.nslow);
   if (c->fast_div && r.nchunks && with_retry) {
     HIPCK(c, hipMalloc(&r.retry, sizeof(int) * r.nchunks));

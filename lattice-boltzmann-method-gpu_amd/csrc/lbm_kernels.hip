@@ -371,9 +371,38 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
+// One cell per lane (small lattices: a wave per 64 cells, so 4x the waves of the chunk path
+// and a quarter of its per-wave latency): plain pulls, exact division, bounce-back slots.
+template <int... Qs>
+__device__ __forceinline__ void pull1_all(float* f, const float* __restrict__ src, int64_t c, int pitch,
+                                          int64_t plane, std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = __builtin_nontemporal_load(src + aidx(c - (Dir<Qs>::x + row_off<Qs>(pitch, plane)), Qs))), ...);
+}
+
+__device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
+  const uint8_t t = a.type[c];
+  const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid &&
+                  !(t & kNeedsMac);
+  if (!in) return 0.0;
+  float f[kQ];
+  pull1_all(f, a.src, c, a.pitch, a.plane, AllQ{});
+  float rho = 0.f;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) rho = rho + f[q];
+  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
+  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
+  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
+  fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
+  fix_store_all(f, a.dst, c, (t & kWallAdj) ? a.links[c] : 0u, a.pitch, a.plane, AllQ{});
+  if (a.store_all_macros) {
+    a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
+  }
+  return (double)sqrtf(ux * ux + uy * uy + uz * uz);
+}
+
 // ---- the step kernel -------------------------------------------------------------------
 
-template <bool FAST>
+template <bool FAST, bool QUARTER>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -388,7 +417,12 @@ __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
     const int b = (int)blockIdx.x - a.nee_blocks;  // nee_blocks is a multiple of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
-    if (idx < a.nchunks) acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
+    if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
+      if ((idx >> 2) < a.nchunks)
+        acc = process_cell1(a, (int64_t)a.chunks[idx >> 2] * kChunk + (idx & 3) * 64 + lane);
+    } else if (idx < a.nchunks) {
+      acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
+    }
     slot += a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
     slot = blockIdx.x;
@@ -726,8 +760,9 @@ bool verify_fast_div(float tau) {
 }
 
 // chunk blocks of k_step: a multiple of the 8 XCDs (see k_step)
-int main_grid(int nchunks) {
-  return nchunks ? std::max(8, ((nchunks + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
+int main_grid(int nchunks, bool quarter) {
+  const int waves = quarter ? 4 * nchunks : nchunks;
+  return nchunks ? std::max(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
 }
 // NEE blocks of k_step (first in the grid): a multiple of 8 so the chunk blocks keep their XCD
 int nee_grid(int n) { return (n + 8 * kBlock - 1) / (8 * kBlock) * 8; }
@@ -739,10 +774,12 @@ constexpr size_t kOccupancyLds = 56 * 1024;
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   const dim3 grid(a.main_blocks + a.nee_blocks);
-  if (a.fast_div)
-    hipLaunchKernelGGL(k_step<true>, grid, dim3(kBlock), kOccupancyLds, s, a);
+  if (a.quarter)  // latency-bound sizes: as many resident waves as the registers allow
+    hipLaunchKernelGGL((k_step<false, true>), grid, dim3(kBlock), 0, s, a);
+  else if (a.fast_div)
+    hipLaunchKernelGGL((k_step<true, false>), grid, dim3(kBlock), kOccupancyLds, s, a);
   else
-    hipLaunchKernelGGL(k_step<false>, grid, dim3(kBlock), kOccupancyLds, s, a);
+    hipLaunchKernelGGL((k_step<false, false>), grid, dim3(kBlock), kOccupancyLds, s, a);
   return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ struct MainArgs {
   const int* chunks;    // active chunk ids
   int nchunks;
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
+  int quarter;          // 1: one cell per lane, a wave per 64-cell quarter chunk (small lattices)
   int pitch;
   int64_t plane;
   int64_t c_lo, c_hi;   // cell ranges of this launch, [c_lo, c_hi) and [c_lo2, c_hi2) (the
@@ -101,7 +102,8 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
-int main_grid(int nchunks);
+int main_grid(int nchunks, bool quarter);
+constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
 int nee_grid(int n);
 constexpr int kReduceBlocks = 256;
 // partial sums -> conv->s_local (deterministic two-level tree: kReduceBlocks blocks sum

@@ -36,3 +36,11 @@ def lbm():
 def gpu(lbm):
     lbm.require_gpu()
     return lbm
+
+
+@pytest.fixture(params=["4", "1"], ids=["4cells", "1cell"])
+def cells_per_lane(request, monkeypatch):
+    """Run a parity test through both stream-collide paths: four cells per lane (the
+    bandwidth path) and one cell per lane (what small lattices use by default)."""
+    monkeypatch.setenv("LBM_CELLS_PER_LANE", request.param)
+    return int(request.param)

@@ -44,7 +44,7 @@ def assert_residuals(hg, ho):
 
 
 @pytest.mark.parametrize("n,steps", [(16, [1, 1, 5, 40]), (32, [1, 3, 100]), (64, [2, 150])])
-def test_ldc_bitwise(gpu, oracle, n, steps):
+def test_ldc_bitwise(gpu, oracle, n, steps, cells_per_lane):
     from lbm_amd import cases
     lat, geo = cases.ldc(n)
     o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
@@ -55,11 +55,12 @@ def test_ldc_bitwise(gpu, oracle, n, steps):
         assert_residuals(hg, ho)
 
 
-def test_fast_division_domain_retry(gpu, oracle):
+def test_fast_division_domain_retry(gpu, oracle, monkeypatch):
     """Populations outside the fast quotient's proven domain (a tiny f, a huge f) make their
     waves re-run on the exact-division path in the same step: still bit-identical, and the
     re-done chunks are counted.  Cells chosen next to the lid (NEE fix-up) and a wall."""
     from lbm_amd import cases
+    monkeypatch.setenv("LBM_CELLS_PER_LANE", "4")  # the fast division lives on the 4-cell path
     n = 32
     lat, geo = cases.ldc(n)
     assert lat.numerics()["fast_div"]
@@ -103,7 +104,7 @@ def test_initial_state_bitwise(gpu, oracle):
 
 @pytest.mark.parametrize("shape,steps", [((32, 32, 32), [1, 2, 60]), ((24, 40, 24), [1, 90]),
                                          ((64, 64, 64), [1, 120])])
-def test_poiseuille_bitwise(gpu, oracle, shape, steps):
+def test_poiseuille_bitwise(gpu, oracle, shape, steps, cells_per_lane):
     from lbm_amd import cases
     nx, ny, nz = shape
     lat, geo = cases.poiseuille(nx, ny, nz)
@@ -116,7 +117,7 @@ def test_poiseuille_bitwise(gpu, oracle, shape, steps):
 
 
 @pytest.mark.parametrize("block", [0, 1])
-def test_bifurcation_bitwise(gpu, oracle, block):
+def test_bifurcation_bitwise(gpu, oracle, block, cells_per_lane):
     from lbm_amd import cases
     lat, geo, inl, outl = cases.bifurcation(block)
     o = oracle.Oracle(oracle.MASK, geo, 0.55, inlet_uy=inl, outlet_uy=outl)
@@ -188,7 +189,7 @@ def test_convergence_loop(gpu, oracle):
 
 
 @pytest.mark.parametrize("nslabs", [2, 3])
-def test_loopback_slabs_bitwise(gpu, nslabs):
+def test_loopback_slabs_bitwise(gpu, nslabs, cells_per_lane):
     """z-slab decomposition with halo exchange (5 populations per face) == one domain."""
     from lbm_amd import cases, initial_fields, Lattice, LBM_CASE_POISEUILLE, LBM_INIT_EXPANDED
     import lbm_amd
@@ -298,7 +299,7 @@ def test_fast_division_retry_large(gpu, oracle):
 
 
 @pytest.mark.parametrize("shape", [(24, 14, 12), (40, 22, 18)])
-def test_generic_boundaries_bitwise(gpu, oracle, shape):
+def test_generic_boundaries_bitwise(gpu, oracle, shape, cells_per_lane):
     """LBM_CASE_GENERIC: inlet (+x, velocity + rho, per-cell table), outlet (-x, velocity),
     side outlet (-z) and a pressure patch (+y) -- coronary.cu:716-944's scheme on every kind
     of face -- bit for bit against the oracle's generic restatement."""
@@ -315,7 +316,7 @@ def test_generic_boundaries_bitwise(gpu, oracle, shape):
 
 
 @pytest.mark.parametrize("shape", [(37, 29, 23), (13, 11, 7), (66, 9, 31)])
-def test_ragged_shapes_bitwise(gpu, oracle, shape):
+def test_ragged_shapes_bitwise(gpu, oracle, shape, cells_per_lane):
     """Extents that are not multiples of 4 (row padding, row shift, chunks straddling rows
     and planes) and very flat boxes."""
     from lbm_amd import cases
