@@ -348,3 +348,26 @@ def test_thin_slabs_loopback(gpu):
     for z0, z1, lat in slabs:
         for a, b in zip(lat.macros(), ref):
             assert np.array_equal(a.view(np.uint32), b[z0:z1].view(np.uint32))
+
+
+def test_rccl_single_rank_step_path(gpu, cells_per_lane):
+    """lbm_attach_rccl with one rank: the multi-GPU step (edge planes then interior on two
+    streams, halo pack/unpack, residual all-reduce + device finisher) with no peers -- must
+    match the single-domain step bit for bit, residuals included."""
+    from lbm_amd import cases
+    import lbm_amd
+    a = cases.ldc_device(40, 36, 44)
+    b = cases.ldc_device(40, 36, 44)
+    b.attach_rccl(lbm_amd.rccl_unique_id(), 0, 1)
+    ha = a.step(35)
+    hb = b.step(35)
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32))
+    for x, y in zip(a.macros(), b.macros()):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    # convergence control through the RCCL finisher
+    a.set_convergence(True, max_it=60, stag_max=50, tol=1e-6)
+    b.set_convergence(True, max_it=60, stag_max=50, tol=1e-6)
+    a.step(100)
+    b.step(100)
+    assert a.state()["k"] == b.state()["k"] == 61
+    b.close()
