@@ -627,10 +627,10 @@ const int* qset(lbm_ctx* c, int which) { return c->qsets + (which == 0 ? 0 : whi
 
 // pack this slab's outgoing faces of buffer b: the top plane's up-going populations and the
 // bottom plane's down-going ones (all 19 when `all`)
-int pack_faces(lbm_ctx* c, int b, bool all, hipStream_t st) {
+int pack_faces(lbm_ctx* c, int b, bool all, bool to_dn, bool to_up, hipStream_t st) {
   const int nq = all ? kQ : 5;
-  HIPCK(c, launch_pack(c->buf[b], c->send_up, c->L.nz, c->L.plane, all ? qset(c, 2) : qset(c, 0), nq, st));
-  HIPCK(c, launch_pack(c->buf[b], c->send_dn, 1, c->L.plane, all ? qset(c, 2) : qset(c, 1), nq, st));
+  if (to_up) HIPCK(c, launch_pack(c->buf[b], c->send_up, c->L.nz, c->L.plane, all ? qset(c, 2) : qset(c, 0), nq, st));
+  if (to_dn) HIPCK(c, launch_pack(c->buf[b], c->send_dn, 1, c->L.plane, all ? qset(c, 2) : qset(c, 1), nq, st));
   return LBM_OK;
 }
 
@@ -653,9 +653,11 @@ int rccl_exchange(lbm_ctx* c, int b, bool all) {
   const size_t cnt = (size_t)(all ? kQ : 5) * c->L.plane;
   const int up = c->rank + 1 < c->nranks ? c->rank + 1 : -1;
   const int dn = c->rank > 0 ? c->rank - 1 : -1;
-  RCK(pack_faces(c, b, all, c->s_comp));
+  // the edge planes are done on s_comp; packing, the transfers and the unpack run on s_comm,
+  // beside the interior launch
   HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
   HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
+  RCK(pack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
   NCCK(c, ncclGroupStart());
   if (up >= 0) {
     NCCK(c, ncclSend(c->send_up, cnt, ncclFloat, up, c->comm, c->s_comm));
@@ -699,13 +701,13 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     RCK(run_range(c, c->edge, h, store_all, c->s_comp, false));
     RCK(rccl_exchange(c, (h + 1) & 1, false));
     RCK(run_range(c, c->mid, h, store_all, c->s_comp, true, &a));
-    // the previous step's all-reduce has read s_local / the finisher has run
-    HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
+    // this rank's sum goes to the step-parity slot: the all-reduce of step h - 2, which read
+    // the same slot, precedes exchange(h - 1) on s_comm, and s_comp waited for that at the top
     HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, a.fast_div ? &a : nullptr,
-                           c->retried, c->s_comp));
+                           c->retried, c->s_comp, &c->conv->s_slot[h & 1]));
     HIPCK(c, hipEventRecord(c->ev_sum, c->s_comp));
     HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_sum, 0));
-    NCCK(c, ncclAllReduce(&c->conv->s_local, &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
+    NCCK(c, ncclAllReduce(&c->conv->s_slot[h & 1], &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
     HIPCK(c, launch_finish_global(c->conv, want_hist ? c->hist + s : nullptr, c->s_comm));
     HIPCK(c, hipEventRecord(c->ev_fin, c->s_comm));
   }
@@ -899,7 +901,7 @@ __global__ void k_sum_locals(ConvState** convs, int n) {
 
 // slab i's packed top face -> slab i+1's bottom ghost; slab i+1's bottom face -> slab i's top
 int loopback_exchange(lbm_ctx** cs, int n, int b, bool all, hipStream_t st) {
-  for (int i = 0; i < n; ++i) RCK(pack_faces(cs[i], b, all, st));
+  for (int i = 0; i < n; ++i) RCK(pack_faces(cs[i], b, all, i > 0, i + 1 < n, st));
   const size_t bytes = sizeof(float) * (all ? kQ : 5) * (size_t)cs[0]->L.plane;
   for (int i = 0; i + 1 < n; ++i) {
     HIPCK(cs[i], hipMemcpyAsync(cs[i + 1]->recv_dn, cs[i]->send_up, bytes, hipMemcpyDeviceToDevice, st));

@@ -474,15 +474,15 @@ __global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict_
 }
 
 __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__ slices, int n, ConvState* cv,
-                                                      float* hist_slot, int finish, int* retry_count,
-                                                      unsigned long long* retried_total) {
+                                                      double* local_out, float* hist_slot, int finish,
+                                                      int* retry_count, unsigned long long* retried_total) {
   __shared__ double red[4];
   if (cv->stopped) return;
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += slices[i];  // fixed order
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
-    cv->s_local = s;
+    *local_out = s;
     if (finish) residual_logic(cv, s, hist_slot);
     if (retry_count) {
       const int nq = *retry_count;
@@ -498,7 +498,8 @@ __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__
 // in one block -- one launch less per step where launches dominate (LDC 64^3: ~26 us/step)
 constexpr int kReduceOneMax = 16384;
 __global__ __launch_bounds__(512) void k_reduce_one(const double* __restrict__ partial, int n, ConvState* cv,
-                                                     float* hist_slot, int finish, const MainArgs m, int retry,
+                                                     double* local_out, float* hist_slot, int finish,
+                                                     const MainArgs m, int retry,
                                                      unsigned long long* retried_total) {
   __shared__ double red[8];
   if (cv->stopped) return;
@@ -518,7 +519,7 @@ __global__ __launch_bounds__(512) void k_reduce_one(const double* __restrict__ p
   r = block_sum(r, red);
   if (threadIdx.x == 0) {
     s += r;
-    cv->s_local = s;
+    *local_out = s;
     if (finish) residual_logic(cv, s, hist_slot);
     if (nq) {
       *retried_total += (unsigned long long)nq;
@@ -784,18 +785,20 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot, int finish,
-                         const MainArgs* retry, unsigned long long* retried_total, hipStream_t s) {
+                         const MainArgs* retry, unsigned long long* retried_total, hipStream_t s,
+                         double* local_out) {
+  if (!local_out) local_out = &conv->s_local;
   MainArgs m{};
   if (retry) m = *retry;
   const int do_retry = (retry && retry->retry_count) ? 1 : 0;
   if (n <= kReduceOneMax) {
-    hipLaunchKernelGGL(k_reduce_one, dim3(1), dim3(512), 0, s, partial, n, conv, hist_slot, finish, m, do_retry,
-                       retried_total);
+    hipLaunchKernelGGL(k_reduce_one, dim3(1), dim3(512), 0, s, partial, n, conv, local_out, hist_slot, finish, m,
+                       do_retry, retried_total);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv, m, do_retry);
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, 2 * kReduceBlocks, conv, hist_slot, finish,
-                     do_retry ? retry->retry_count : nullptr, retried_total);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, 2 * kReduceBlocks, conv, local_out, hist_slot,
+                     finish, do_retry ? retry->retry_count : nullptr, retried_total);
   return hipGetLastError();
 }
 

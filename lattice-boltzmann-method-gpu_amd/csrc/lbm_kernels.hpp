@@ -90,6 +90,7 @@ bool verify_fast_div(float tau);
 struct ConvState {      // device-resident reference main-loop state (ldc.cu:613-685)
   double s_local;       // this rank's sum of |u| for the last step
   double s_global;      // after the cross-rank all-reduce
+  double s_slot[2];     // RCCL path: this rank's sum by step parity (the all-reduce's input)
   float sum_current;    // S_{k-1} as float (ldc.cu:683)
   float residual;       // last residual
   int k;                // steps executed
@@ -112,7 +113,8 @@ constexpr int kReduceBlocks = 256;
 // fast_div queue the slice blocks first re-do with the exact division (their |u| sums join
 // the tree); the final block empties the queue and counts it into *retried_total.
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot,
-                         int finish, const MainArgs* retry, unsigned long long* retried_total, hipStream_t s);
+                         int finish, const MainArgs* retry, unsigned long long* retried_total, hipStream_t s,
+                         double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
 
 // halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack
