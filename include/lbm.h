@@ -113,6 +113,12 @@ typedef struct {
   /* LBM_CASE_GENERIC: the boundary codes (at most 16; copied at lbm_create). */
   const lbm_bc_code* bc_codes;
   int n_bc_codes;
+  /* LBM_CASE_MASK with geo == NULL: the raw geo.txt mask (values 0..255, raster x fastest, one
+   * byte per cell); geo_pre (bifurcation.cu:63-239: wall/fluid erosion, inlet/outlet rows,
+   * ghost marking) runs on the device and the codes never exist on the host.  Planes: nz, or
+   * nz + 6 with halo_planes = 1 (global z_offset-3 .. z_offset+nz+2; planes outside the global
+   * box are never read).  Requires ny >= 5. */
+  const uint8_t* mask;
 } lbm_desc;
 
 /* Status / version */
@@ -130,6 +136,11 @@ int lbm_init_equilibrium(lbm_ctx* ctx, int form, const float* rho, const float* 
                          const float* uy, const float* uz);
 /* LDC initial state of ldc.cu:504-580 generated on the device (no host arrays). */
 int lbm_init_ldc(lbm_ctx* ctx);
+/* The case's own initialize() on the device, no host arrays: LBM_CASE_LDC as lbm_init_ldc;
+ * LBM_CASE_MASK as bifurcation.cu:329-427 (rho = 1, u = 0, u_y of code-2 cells in row y = 1
+ * and code-3 cells in row y = ny-2 from bc_inlet_uy / bc_outlet_uy, expanded equilibrium).
+ * Other cases: LBM_ERR_ARG. */
+int lbm_init_case(lbm_ctx* ctx);
 /* Exact initial populations, SoA [19][nz][ny][nx] (into both buffers); resets the step count. */
 int lbm_set_f(lbm_ctx* ctx, const float* f_soa);
 
@@ -151,6 +162,10 @@ int lbm_get_macros(lbm_ctx* ctx, float* rho, float* ux, float* uy, float* uz);
 /* Populations of the last step (the next step's source), SoA [19][nz][ny][nx]; only fluid
  * cells carry reference-defined values. */
 int lbm_get_f(lbm_ctx* ctx, float* f_soa);
+/* The reference mask codes this context runs on (geo_pre's output: 0 unused, -1 ghost, 1 wall,
+ * 2 inlet, 3 outlet / lid, 4 or 3 fluid ...), raster nx*ny*nz over the local planes -- the
+ * device-built codes of a mask or LDC context, the ingested ones otherwise. */
+int lbm_get_geo(lbm_ctx* ctx, int8_t* geo);
 
 /* Sizes: cells in the box, fluid cells, and the bytes one step moves algorithmically
  * (152 B per fluid cell: 19 fp32 loads + 19 fp32 stores). */

@@ -25,8 +25,9 @@ void lbmh_geo_mask(int nx, int ny, int nz, const int32_t* raw, int8_t* geo); /* 
 long lbmh_read_geo_txt(const char* path, int nx, int ny, int nz, int32_t* raw);
 /* bc.txt (bifurcation.cu:294-325): block `inlet_block` is read as the inlet u_y on code-2 cells
  * of the y=1 plane, the next block as the outlet u_y on code-3 cells of y=ny-2 (inlet_block = 0
- * reproduces the shipped code; 1 reads the block that matches the shipped inlet).  Returns the
- * number of tokens consumed (< 0: cannot open). */
+ * reproduces the shipped code; 1 reads the block that matches the shipped inlet).  geo NULL:
+ * the tables are not masked (for lbm_desc.mask contexts, whose lbm_init_case masks by code).
+ * Returns the number of tokens consumed (< 0: cannot open). */
 long lbmh_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* geo, int inlet_block,
                       float* inlet_uy, float* outlet_uy);
 /* index_transform (Poiseulle.cu:257-271): compact ids in z,y,x order over geo != 0 (else -1).

@@ -58,6 +58,8 @@ struct lbm_ctx {
   float* buf[2] = {nullptr, nullptr};  // past the guard chunk
   uint8_t* type = nullptr;
   uint32_t* links = nullptr;
+  int8_t* codes = nullptr;               // reference codes per storage cell (lbm_get_geo)
+  float *bc_in = nullptr, *bc_out = nullptr;  // inlet / outlet u_y tables (lbm_init_case)
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
   Range whole, edge, mid;  // single domain: whole; slabs: both edge planes (one launch), interior
   double* partial_all = nullptr;
@@ -323,8 +325,13 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     g_create_error = "invalid lattice description";
     return LBM_ERR_ARG;
   }
-  if (!d.geo && d.case_kind != LBM_CASE_LDC) {
-    g_create_error = "geo == NULL is only supported for LBM_CASE_LDC";
+  const bool dev_mask = !d.geo && d.mask;
+  if (!d.geo && d.case_kind != LBM_CASE_LDC && !(dev_mask && d.case_kind == LBM_CASE_MASK)) {
+    g_create_error = "geo == NULL is only supported for LBM_CASE_LDC, or LBM_CASE_MASK with a mask";
+    return LBM_ERR_ARG;
+  }
+  if (dev_mask && (d.ny < 5 || (!d.halo_planes && d.nz_global > 0 && (d.nz_global != d.nz || d.z_offset != 0)))) {
+    g_create_error = "device mask build: needs ny >= 5, and halo_planes = 1 for a slab";
     return LBM_ERR_ARG;
   }
   lbm_ctx* c = new lbm_ctx();
@@ -333,6 +340,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   c->d.bc_inlet_uy = nullptr;
   c->d.bc_outlet_uy = nullptr;
   c->d.bc_codes = nullptr;
+  c->d.mask = nullptr;
   for (int k = 0; k < d.n_bc_codes; ++k) {
     const lbm_bc_code& b = d.bc_codes[k];
     if (b.face < 0 || b.face > 5 || b.kind < 0 || b.kind > 2 || b.code == 1 || b.code == 4 || b.code < -128 ||
@@ -416,9 +424,34 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   // ---- geometry: reference codes per linear cell -> type bytes ----
   int8_t* dcodes = nullptr;
   CK(hipMalloc(&dcodes, L.ncell));
+  c->codes = dcodes;  // kept for lbm_get_geo (1 B per cell)
   CK(hipMemsetAsync(dcodes, 0, L.ncell, c->s_comp));
   float *din = nullptr, *dout = nullptr;
-  if (desc->geo) {
+  if (dev_mask) {
+    // geo_pre on the device: upload the raw mask (1 B/cell), pick the row shift from the
+    // device-built codes, then write the codes of every storage cell
+    const int pad = d.halo_planes ? 3 : 0, lo = d.halo_planes ? -1 : 0, hi = d.halo_planes ? d.nz + 1 : d.nz;
+    const int64_t mbytes = (int64_t)d.nx * d.ny * (d.nz + 2 * pad);
+    uint8_t* dmask = nullptr;
+    unsigned long long* dh = nullptr;
+    CK(hipMalloc(&dmask, mbytes));
+    CK(hipMemcpy(dmask, desc->mask, mbytes, hipMemcpyHostToDevice));
+    const int zbase = d.z_offset - pad;
+    if (d.x_align == 0) {
+      unsigned long long hh[4];
+      CK(hipMalloc(&dh, sizeof(hh)));
+      CK(hipMemsetAsync(dh, 0, sizeof(hh), c->s_comp));
+      CK(launch_mask_hist(dmask, d.nx, d.ny, c->d.nz_global, zbase, d.z_offset + lo, d.z_offset + hi, dh, c->s_comp));
+      CK(hipMemcpyAsync(hh, dh, sizeof(hh), hipMemcpyDeviceToHost, c->s_comp));
+      CK(hipStreamSynchronize(c->s_comp));
+      CK(hipFree(dh));
+      L.xshift = (int)(std::max_element(hh, hh + 4) - hh);
+    }
+    CK(launch_mask_codes(dmask, d.nx, d.ny, c->d.nz_global, zbase, dcodes, L.pitch, L.xshift, L.plane, L.ncell,
+                         d.z_offset, lo, hi, c->s_comp));
+    CK(hipStreamSynchronize(c->s_comp));
+    CK(hipFree(dmask));
+  } else if (desc->geo) {
     std::vector<int8_t> h((size_t)L.ncell, 0);
     const int zlo = d.halo_planes ? -1 : 0, zhi = d.halo_planes ? d.nz + 1 : d.nz;
     for (int z = zlo; z < zhi; ++z)
@@ -433,10 +466,12 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   const int64_t ntab = (int64_t)d.nx * c->d.nz_global;
   if (desc->bc_inlet_uy) {
     CK(hipMalloc(&din, sizeof(float) * ntab));
+    c->bc_in = din;  // kept for lbm_init_case
     CK(hipMemcpy(din, desc->bc_inlet_uy, sizeof(float) * ntab, hipMemcpyHostToDevice));
   }
   if (desc->bc_outlet_uy) {
     CK(hipMalloc(&dout, sizeof(float) * ntab));
+    c->bc_out = dout;
     CK(hipMemcpy(dout, desc->bc_outlet_uy, sizeof(float) * ntab, hipMemcpyHostToDevice));
   }
   GeoArgs g{};
@@ -469,9 +504,6 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   CK(launch_classify(g, c->s_comp));
   CK(launch_flag_fluid(g, c->s_comp));
   CK(hipStreamSynchronize(c->s_comp));
-  CK(hipFree(dcodes));
-  if (din) CK(hipFree(din));
-  if (dout) CK(hipFree(dout));
   for (float* t : bc_tables) CK(hipFree(t));
 
   // ---- work lists: whole domain, and lo edge / hi edge / interior for slabs ----
@@ -522,6 +554,9 @@ void lbm_destroy(lbm_ctx* c) {
   for (Range* r : {&c->whole, &c->edge, &c->mid}) free_range(*r);
   if (c->type) (void)hipFree(c->type);
   if (c->links) (void)hipFree(c->links);
+  if (c->codes) (void)hipFree(c->codes);
+  if (c->bc_in) (void)hipFree(c->bc_in);
+  if (c->bc_out) (void)hipFree(c->bc_out);
   if (c->partial_all) (void)hipFree(c->partial_all);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
@@ -563,6 +598,21 @@ int lbm_init_ldc(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
   HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.xshift, c->L.ny, c->d.lid_u, c->s_comp));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  return reset_state(c);
+}
+
+int lbm_init_case(lbm_ctx* c) {
+  if (!c) return LBM_ERR_ARG;
+  if (c->d.case_kind == LBM_CASE_LDC) return lbm_init_ldc(c);
+  if (c->d.case_kind != LBM_CASE_MASK) {
+    c->err = "lbm_init_case: only LBM_CASE_LDC and LBM_CASE_MASK have a device initialize()";
+    return LBM_ERR_ARG;
+  }
+  HIPCK(c, hipSetDevice(c->d.device));
+  const Layout& L = c->L;
+  HIPCK(c, launch_init_mask(c->buf[0], c->buf[1], c->codes, c->bc_in, c->bc_out, L.nx, L.ny, L.nz, L.pitch, L.xshift,
+                            L.plane, L.ncell, c->d.z_offset, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -788,6 +838,18 @@ int lbm_get_macros(lbm_ctx* c, float* rho, float* ux, float* uy, float* uz) {
           outs[k][((int64_t)z * L.ny + y) * L.nx + x] = ((t[s] & kClassMask) == kFluid) ? h[s] : 0.0f;
         }
   }
+  return LBM_OK;
+}
+
+int lbm_get_geo(lbm_ctx* c, int8_t* geo) {
+  if (!c || !geo) return LBM_ERR_ARG;
+  RCK(lbm_sync(c));
+  const Layout& L = c->L;
+  std::vector<int8_t> h((size_t)L.ncell);
+  HIPCK(c, hipMemcpy(h.data(), c->codes, L.ncell, hipMemcpyDeviceToHost));
+  for (int z = 0; z < L.nz; ++z)
+    for (int y = 0; y < L.ny; ++y)
+      for (int x = 0; x < L.nx; ++x) geo[((int64_t)z * L.ny + y) * L.nx + x] = h[cell_of(L, x, y, z)];
   return LBM_OK;
 }
 

@@ -141,12 +141,12 @@ long lbmh_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* ge
   for (int z = 0; z < nz; ++z)
     for (int x = 0; x < nx; ++x) {
       next(v);
-      inlet_uy[x + (int64_t)z * nx] = geo[b(x, 1, z)] == 2 ? v : 0.0f;
+      inlet_uy[x + (int64_t)z * nx] = (!geo || geo[b(x, 1, z)] == 2) ? v : 0.0f;
     }
   for (int z = 0; z < nz; ++z)
     for (int x = 0; x < nx; ++x) {
       next(v);
-      outlet_uy[x + (int64_t)z * nx] = geo[b(x, ny - 2, z)] == 3 ? v : 0.0f;
+      outlet_uy[x + (int64_t)z * nx] = (!geo || geo[b(x, ny - 2, z)] == 3) ? v : 0.0f;
     }
   std::fclose(f);
   return ntok;

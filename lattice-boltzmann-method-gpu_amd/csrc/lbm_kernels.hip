@@ -709,7 +709,111 @@ __global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift
   }
 }
 
+// ---- geo_pre of a raw mask on the device (bifurcation.cu:63-239) -------------
+// Global coordinates throughout; the mask holds planes zbase .. zbase + mplanes - 1.
+struct MaskGeo {
+  const uint8_t* m;
+  int nx, ny, nzg, zbase;
+};
+
+__device__ __forceinline__ int mraw(const MaskGeo& g, int x, int y, int z) {
+  return g.m[x + (int64_t)g.nx * (y + (int64_t)g.ny * (z - g.zbase))];
+}
+
+// min over the 6 face neighbours (the reference's distance-transform step)
+__device__ __forceinline__ int mmin6(const MaskGeo& g, int x, int y, int z) {
+  int v = min(mraw(g, x + 1, y, z), mraw(g, x - 1, y, z));
+  v = min(v, min(mraw(g, x, y + 1, z), mraw(g, x, y - 1, z)));
+  return min(v, min(mraw(g, x, y, z + 1), mraw(g, x, y, z - 1)));
+}
+
+// the code before ghost marking: y = 0 / ny-1 planes cleared, interior += 3*min6, inlet row
+// y = 1 and outlet row y = ny-2 from the row next to them (requires ny >= 5)
+__device__ int mask_pre(const MaskGeo& g, int x, int y, int z) {
+  if (x < 1 || x > g.nx - 2 || z < 1 || z > g.nzg - 2) return mraw(g, x, y, z);
+  if (y == 0 || y == g.ny - 1) return 0;
+  if (y == 1) {
+    const int in = mraw(g, x, 2, z) + 3 * mmin6(g, x, 2, z);
+    return in == 1 ? 1 : (in == 4 ? 2 : 0);
+  }
+  if (y == g.ny - 2) {
+    const int out = mraw(g, x, g.ny - 3, z) + 3 * mmin6(g, x, g.ny - 3, z);
+    return out == 1 ? 1 : (out == 4 ? 3 : 0);
+  }
+  return mraw(g, x, y, z) + 3 * mmin6(g, x, y, z);
+}
+
+// final code: an unused cell next to an interior wall (code 1) becomes a ghost (-1).  The
+// reference scatters from each wall to its 18 neighbours; only 0 -> -1 changes, so gathering
+// from the 18 neighbours gives the same codes in any order.
+__device__ int mask_code(const MaskGeo& g, int x, int y, int z) {
+  const int v = mask_pre(g, x, y, z);
+  if (v != 0) return v;
+  for (int q = 1; q < kQ; ++q) {
+    const int sx = x - kEx[q], sy = y - kEy[q], sz = z - kEz[q];
+    if (sx >= 1 && sx <= g.nx - 2 && sy >= 1 && sy <= g.ny - 2 && sz >= 1 && sz <= g.nzg - 2 &&
+        mask_pre(g, sx, sy, sz) == 1)
+      return -1;
+  }
+  return 0;
+}
+
+// first fluid (code 4) x of every row of planes z_lo .. z_hi-1 -> hist[x & 3] (choose_xshift)
+__global__ void k_mask_hist(MaskGeo g, int z_lo, int z_hi, unsigned long long* hist) {
+  const int64_t rows = (int64_t)(z_hi - z_lo) * g.ny;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(r % g.ny), z = z_lo + (int)(r / g.ny);
+    if (z < 0 || z >= g.nzg) continue;
+    for (int x = 0; x < g.nx; ++x)
+      if (mask_code(g, x, y, z) == 4) {
+        atomicAdd(&hist[x & 3], 1ull);
+        break;
+      }
+  }
+}
+
+// codes of every storage cell (layout order, as k_ldc_codes); storage planes outside
+// z_lo .. z_hi-1 (local) or outside the global box stay 0
+__global__ void k_mask_codes(MaskGeo g, int8_t* codes, int pitch, int xshift, int64_t plane, int64_t ncell,
+                             int z_offset, int z_lo, int z_hi) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = c + xshift;
+    const int x = (int)(u % pitch);
+    const int y = (int)((u / pitch) % g.ny);
+    const int zl = (int)(u / plane) - 1;
+    const int z = zl + z_offset;
+    int8_t code = 0;
+    if (x < g.nx && zl >= z_lo && zl < z_hi && z >= 0 && z < g.nzg) code = (int8_t)mask_code(g, x, y, z);
+    codes[c] = code;
+  }
+}
+
 // ---- initial state ---------------------------------------------------------------------
+
+// bifurcation.cu:329-427 on the device: rho = 1, u = 0 except u_y of the inlet (code 2, row
+// y = 1) and outlet (code 3, row y = ny-2) cells of the local planes, from the bc tables
+// (x + global z * nx); expanded equilibrium into both buffers
+__global__ void k_init_mask(float* fa, float* fb, const int8_t* codes, const float* in_uy, const float* out_uy, int nx,
+                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = c + xshift;
+    const int x = (int)(u % pitch);
+    const int y = (int)((u / pitch) % ny);
+    const int zl = (int)(u / plane) - 1;
+    float vy = 0.0f;
+    if (x < nx && zl >= 0 && zl < nz) {
+      const int64_t t = x + (int64_t)(zl + z_offset) * nx;
+      if (y == 1 && codes[c] == 2 && in_uy) vy = in_uy[t];
+      if (y == ny - 2 && codes[c] == 3 && out_uy) vy = out_uy[t];
+    }
+    float e[kQ];
+    feq_expanded(1.0f, 0.0f, vy, 0.0f, e);
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) { fa[aidx(c, q)] = e[q]; fb[aidx(c, q)] = e[q]; }
+  }
+}
 
 __global__ void k_init_feq(float* fa, float* fb, int64_t n, int form, const float* rho, const float* ux,
                            const float* uy, const float* uz) {
@@ -842,9 +946,34 @@ hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift
   return hipGetLastError();
 }
 
+hipError_t launch_mask_hist(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int z_lo, int z_hi,
+                            unsigned long long* hist, hipStream_t s) {
+  const MaskGeo g{mask, nx, ny, nz_global, zbase};
+  hipLaunchKernelGGL(k_mask_hist, dim3(grid_for((int64_t)(z_hi - z_lo) * ny, 256)), dim3(256), 0, s, g, z_lo, z_hi,
+                     hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_mask_codes(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int8_t* codes, int pitch,
+                             int xshift, int64_t plane, int64_t ncell, int z_offset, int z_lo, int z_hi,
+                             hipStream_t s) {
+  const MaskGeo g{mask, nx, ny, nz_global, zbase};
+  hipLaunchKernelGGL(k_mask_codes, dim3(grid_for(ncell, 256)), dim3(256), 0, s, g, codes, pitch, xshift, plane, ncell,
+                     z_offset, z_lo, z_hi);
+  return hipGetLastError();
+}
+
 hipError_t launch_init_feq(float* fa, float* fb, int64_t n, int form, const float* rho, const float* ux,
                            const float* uy, const float* uz, hipStream_t s) {
   hipLaunchKernelGGL(k_init_feq, dim3(grid_for(n, 256)), dim3(256), 0, s, fa, fb, n, form, rho, ux, uy, uz);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_mask(float* fa, float* fb, const int8_t* codes, const float* in_uy, const float* out_uy, int nx,
+                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_init_mask, dim3(grid_for(ncell, 256)), dim3(256), 0, s, fa, fb, codes, in_uy, out_uy, nx, ny, nz,
+                     pitch, xshift, plane, ncell, z_offset);
   return hipGetLastError();
 }
 

@@ -158,8 +158,17 @@ hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift
 
 // initial populations from per-cell fields (nullable -> rho 1, u 0); form 0 = LDC wi form,
 // 1 = expanded; writes both buffers for every cell
+// geo_pre of a raw 0/1 mask on the device (bifurcation.cu:63-239): mask planes are global
+// z = zbase .. ; local storage planes z_lo .. z_hi-1 get codes (-1 for the halo plane below)
+hipError_t launch_mask_hist(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int z_lo, int z_hi,
+                            unsigned long long* hist, hipStream_t s);
+hipError_t launch_mask_codes(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int8_t* codes, int pitch,
+                             int xshift, int64_t plane, int64_t ncell, int z_offset, int z_lo, int z_hi, hipStream_t s);
 hipError_t launch_init_feq(float* fa, float* fb, int64_t ncell, int form, const float* rho, const float* ux,
                            const float* uy, const float* uz, hipStream_t s);
+hipError_t launch_init_mask(float* fa, float* fb, const int8_t* codes, const float* in_uy, const float* out_uy, int nx,
+                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
+                            hipStream_t s);
 hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int ny, float lid_u, hipStream_t s);
 
 }  // namespace lbm

@@ -72,14 +72,15 @@ class lbm_desc(C.Structure):
         ("x_align", C.c_int),
         ("bc_codes", C.POINTER(lbm_bc_code)),
         ("n_bc_codes", C.c_int),
+        ("mask", C.POINTER(C.c_uint8)),
     ]
 
 
 # every symbol include/lbm.h and include/lbm_host.h declare (checked by the CPU tests)
 LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
-    "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
-    "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
+    "lbm_init_case", "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
+    "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
 ]
 HOST_SYMBOLS = [
@@ -144,6 +145,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_destroy": (None, [P]),
             "lbm_init_equilibrium": (C.c_int, [P, C.c_int, f32p, f32p, f32p, f32p]),
             "lbm_init_ldc": (C.c_int, [P]),
+            "lbm_init_case": (C.c_int, [P]),
             "lbm_set_f": (C.c_int, [P, f32p]),
             "lbm_set_convergence": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_float]),
             "lbm_step": (C.c_int, [P, C.c_int, f32p, ip]),
@@ -151,6 +153,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_get_state": (C.c_int, [P, ip, ip, ip, f32p, f64p]),
             "lbm_get_macros": (C.c_int, [P, f32p, f32p, f32p, f32p]),
             "lbm_get_f": (C.c_int, [P, f32p]),
+            "lbm_get_geo": (C.c_int, [P, C.POINTER(C.c_int8)]),
             "lbm_get_counts": (C.c_int, [P, i64p, i64p, f64p]),
             "lbm_profile": (C.c_int, [P, C.c_int]),
             "lbm_stats": (C.c_int, [P, f64p, i64p, f64p]),
@@ -205,11 +208,14 @@ def geo_mask(raw: np.ndarray) -> np.ndarray:
     return g
 
 
-def read_bc_txt(path: str, geo: np.ndarray, inlet_block: int = 0):
-    nz, ny, nx = geo.shape
+def read_bc_txt(path: str, geo, inlet_block: int = 0):
+    """geo: the codes (entries off code-2 / code-3 cells are zeroed), or a (nz, ny, nx) shape
+    for the unmasked tables (the device-built mask path masks them itself)."""
+    g = None if isinstance(geo, tuple) else np.ascontiguousarray(geo, np.int8)
+    nz, ny, nx = geo if g is None else g.shape
     inl = np.zeros((nz, nx), np.float32)
     out = np.zeros((nz, nx), np.float32)
-    n = host_lib().lbmh_read_bc_txt(path.encode(), nx, ny, nz, _ptr(np.ascontiguousarray(geo), C.c_int8),
+    n = host_lib().lbmh_read_bc_txt(path.encode(), nx, ny, nz, _ptr(g, C.c_int8),
                                     inlet_block, _ptr(inl, C.c_float), _ptr(out, C.c_float))
     if n < 0:
         raise LbmError(f"cannot read {path}")
@@ -279,7 +285,9 @@ class Lattice:
     def __init__(self, case_kind: int, shape, tau: float, geo: np.ndarray | None = None, *,
                  halo_planes: bool = False, lid_u_val: float | None = None, inlet_uy=None, outlet_uy=None,
                  device: int = 0, z_offset: int = 0, nz_global: int | None = None, x_align: int = 0,
-                 bc_codes=None):
+                 bc_codes=None, mask: np.ndarray | None = None):
+        """mask (LBM_CASE_MASK, geo None): raw geo.txt mask, uint8 [nz (+6 with halo_planes)][ny][nx];
+        geo_pre runs on the device (lbm_desc.mask)."""
         nz, ny, nx = shape
         self.shape = (nz, ny, nx)
         self.case_kind = case_kind
@@ -295,6 +303,13 @@ class Lattice:
                 raise LbmError(f"geo shape {g.shape} != {want}")
             self._keep.append(g)
             d.geo = _ptr(g, C.c_int8)
+        if mask is not None:
+            m = np.ascontiguousarray(mask, np.uint8)
+            want = (nz + 6 if halo_planes else nz, ny, nx)
+            if m.shape != want:
+                raise LbmError(f"mask shape {m.shape} != {want}")
+            self._keep.append(m)
+            d.mask = _ptr(m, C.c_uint8)
         d.halo_planes = 1 if halo_planes else 0
         d.lid_u = lid_u() if lid_u_val is None else lid_u_val
         for name, tab in (("bc_inlet_uy", inlet_uy), ("bc_outlet_uy", outlet_uy)):
@@ -349,6 +364,16 @@ class Lattice:
 
     def init_ldc(self):
         self._ck(lbm_lib().lbm_init_ldc(self.h), "lbm_init_ldc")
+
+    def init_case(self):
+        """The case's initialize() on the device (LDC, MASK)."""
+        self._ck(lbm_lib().lbm_init_case(self.h), "lbm_init_case")
+
+    def geo(self) -> np.ndarray:
+        """The reference mask codes of the local planes, int8 [nz][ny][nx]."""
+        a = np.zeros(self.shape, np.int8)
+        self._ck(lbm_lib().lbm_get_geo(self.h, _ptr(a, C.c_int8)), "lbm_get_geo")
+        return a
 
     def set_f(self, f: np.ndarray):
         a = np.ascontiguousarray(f, np.float32)

@@ -120,3 +120,39 @@ def slab_geo(geo: np.ndarray, z0: int, z1: int) -> np.ndarray:
         if 0 <= z < nz:
             out[k] = geo[z]
     return out
+
+
+def slab_mask(raw: np.ndarray, z0: int, z1: int) -> np.ndarray:
+    """Planes z0-3 .. z1+2 of a global raw mask, uint8 (lbm_desc.mask of a halo slab: geo_pre of
+    the halo planes reads two planes beyond them); planes outside the box are zero."""
+    nz, ny, nx = raw.shape
+    out = np.zeros((z1 - z0 + 6, ny, nx), np.uint8)
+    for k, z in enumerate(range(z0 - 3, z1 + 3)):
+        if 0 <= z < nz:
+            out[k] = raw[z]
+    return out
+
+
+def mask_device(raw: np.ndarray, inlet_uy=None, outlet_uy=None, tau: float = BIF_TAU, device: int = 0,
+                z_offset: int = 0, nz_global: int | None = None, halo_planes: bool = False, x_align: int = 0):
+    """bifurcation.cu's set-up with geo_pre on the device: `raw` is the geo.txt
+    mask (uint8; with halo_planes the slab_mask of this slab), the codes are built and the
+    initial state is evaluated on the device (lbm_init_case).  inlet_uy / outlet_uy are the
+    bc.txt tables, masked or not."""
+    m = np.ascontiguousarray(raw, np.uint8)
+    nz = m.shape[0] - (6 if halo_planes else 0)
+    lat = Lattice(LBM_CASE_MASK, (nz, m.shape[1], m.shape[2]), tau, None, mask=m, inlet_uy=inlet_uy,
+                  outlet_uy=outlet_uy, device=device, z_offset=z_offset, nz_global=nz_global,
+                  halo_planes=halo_planes, x_align=x_align)
+    lat.init_case()
+    return lat
+
+
+def bifurcation_device(inlet_block: int = 0, geo_path: str | None = None, bc_path: str | None = None,
+                       device: int = 0):
+    """bifurcation() with the mask codes built and the state initialised on the device."""
+    geo_path = geo_path or os.path.join(BIF_DIR, "geo.txt")
+    bc_path = bc_path or os.path.join(BIF_DIR, "bc.txt")
+    raw = read_geo_txt(geo_path, BIF_SHAPE)
+    _, inl, outl = read_bc_txt(bc_path, tuple(BIF_SHAPE), inlet_block)
+    return mask_device(raw.astype(np.uint8), inl, outl, device=device), raw

@@ -79,6 +79,17 @@ def test_invalid_descriptions_rejected(lbm):
         lbm.Lattice(lbm.LBM_CASE_POISEUILLE, (8, 8, 8), 0.58, None)
     with pytest.raises(lbm.LbmError, match="invalid lattice description"):
         lbm.Lattice(lbm.LBM_CASE_LDC, (8, 8, 8), 0.55, None, x_align=7)
+    # device mask build: MASK case only, ny >= 5, slabs need halo planes
+    import numpy as np
+    with pytest.raises(lbm.LbmError, match="geo == NULL"):
+        lbm.Lattice(lbm.LBM_CASE_POISEUILLE, (8, 8, 8), 0.58, None, mask=np.ones((8, 8, 8), np.uint8))
+    with pytest.raises(lbm.LbmError, match="ny >= 5"):
+        lbm.Lattice(lbm.LBM_CASE_MASK, (8, 4, 8), 0.55, None, mask=np.ones((8, 4, 8), np.uint8))
+    with pytest.raises(lbm.LbmError, match="halo_planes"):
+        lbm.Lattice(lbm.LBM_CASE_MASK, (8, 8, 8), 0.55, None, mask=np.ones((8, 8, 8), np.uint8), z_offset=8,
+                    nz_global=16)
+    with pytest.raises(lbm.LbmError, match="mask shape"):
+        lbm.Lattice(lbm.LBM_CASE_MASK, (8, 8, 8), 0.55, None, mask=np.ones((8, 8, 8), np.uint8), halo_planes=True)
 
 
 def test_drivers_built():

@@ -1,0 +1,121 @@
+"""geo_pre on the device (lbm_desc.mask): the codes the device builds from a raw
+mask equal the oracle's restatement of bifurcation.cu:63-239 (orc_geo_mask, pinned by the
+reference's geo.txt counts), cell for cell, for the shipped geometry, synthetic vessel masks of
+ragged shapes, random noise masks and halo slabs; lattices built and initialised that way step
+bit for bit like the oracle and like the host-ingested path."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def vessel_mask(shape, seed, nballs=5):
+    """A tube along y with random bulges, 0 on the outer x / z layers (as geo.txt)."""
+    nz, ny, nx = shape
+    rng = np.random.default_rng(seed)
+    z, y, x = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    r = min(nx, nz) / 3.2
+    m = ((x - (nx - 1) / 2) ** 2 + (z - (nz - 1) / 2) ** 2) <= r * r
+    for _ in range(nballs):
+        c = rng.uniform([0, 0, 0], [nz, ny, nx])
+        rr = rng.uniform(1.5, min(nx, nz) / 3)
+        m |= ((z - c[0]) ** 2 + (y - c[1]) ** 2 + (x - c[2]) ** 2) <= rr * rr
+    m = m.astype(np.uint8)
+    m[:, :, 0] = m[:, :, -1] = 0
+    m[0] = m[-1] = 0
+    return m
+
+
+def inlet_tables(shape, seed):
+    nz, ny, nx = shape
+    rng = np.random.default_rng(seed)
+    return (rng.uniform(0.01, 0.05, (nz, nx)).astype(np.float32),
+            rng.uniform(0.01, 0.05, (nz, nx)).astype(np.float32))
+
+
+def test_device_geo_bifurcation(gpu, oracle):
+    from lbm_amd import cases
+    lat, raw = cases.bifurcation_device(1)
+    want = oracle.geo_mask(raw)
+    got = lat.geo()
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} codes differ"
+    # the host-ingested context reports the codes it was given
+    host, geo, _, _ = cases.bifurcation(1)
+    assert np.array_equal(host.geo(), geo)
+    assert lat.counts() == host.counts()
+
+
+@pytest.mark.parametrize("shape", [(23, 31, 37), (12, 9, 13), (30, 40, 66)])
+def test_device_geo_vessels_and_noise(gpu, oracle, shape):
+    from lbm_amd import cases
+    for raw in (vessel_mask(shape, 1), (np.random.default_rng(2).random(shape) < 0.75).astype(np.uint8)):
+        lat = cases.mask_device(raw)
+        want = oracle.geo_mask(raw.astype(np.int32))
+        got = lat.geo()
+        assert np.array_equal(got, want), f"{shape}: {np.count_nonzero(got != want)} codes differ"
+        lat.close()
+
+
+@pytest.mark.parametrize("shape", [(23, 31, 37), (30, 40, 66)])
+def test_device_mask_lattice_bitwise(gpu, oracle, shape, cells_per_lane):
+    """Device codes + device initialize() vs the oracle (and the host path) over 60 steps."""
+    from lbm_amd import cases, geo_mask, initial_fields, Lattice, LBM_CASE_MASK, LBM_INIT_EXPANDED
+    raw = vessel_mask(shape, 3)
+    inl, outl = inlet_tables(shape, 4)
+    dev = cases.mask_device(raw, inl, outl, tau=0.55)
+    geo = geo_mask(raw.astype(np.int32))
+    assert np.array_equal(dev.geo(), geo)
+    inl_m = np.where(geo[:, 1, :] == 2, inl, 0).astype(np.float32)
+    outl_m = np.where(geo[:, -2, :] == 3, outl, 0).astype(np.float32)
+    host = Lattice(LBM_CASE_MASK, shape, 0.55, geo, inlet_uy=inl_m)
+    host.init_equilibrium(LBM_INIT_EXPANDED, *initial_fields(2, geo, inl_m, outl_m))
+    o = oracle.Oracle(oracle.MASK, geo, 0.55, inlet_uy=inl_m, outlet_uy=outl_m)
+    for s in (1, 59):
+        hd, hh = dev.step(s), host.step(s)
+        o.step(s)
+        assert np.array_equal(hd.view(np.uint32), hh.view(np.uint32))
+        assert_bitwise(dev, o, geo, 2, f"device mask {shape}")
+    fd, fh = dev.f(), host.f()
+    m = geo == 4
+    assert np.array_equal(fd[:, m].view(np.uint32), fh[:, m].view(np.uint32))
+
+
+def test_device_bifurcation_matches_host(gpu):
+    from lbm_amd import cases
+    dev, _ = cases.bifurcation_device(1)
+    host, geo, _, _ = cases.bifurcation(1)
+    hd, hh = dev.step(300), host.step(300)
+    assert np.array_equal(hd.view(np.uint32), hh.view(np.uint32))
+    for a, b in zip(dev.macros(), host.macros()):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("nslabs", [2, 3])
+def test_device_mask_slabs(gpu, nslabs):
+    """Halo slabs built from slab_mask (3 extra planes each side): each slab's codes are the
+    global codes of its planes, and the loopback slab run equals the single domain."""
+    from lbm_amd import cases, geo_mask, x_align_for, LBM_CASE_MASK
+    import lbm_amd
+    shape = (29, 31, 37)
+    nz = shape[0]
+    raw = vessel_mask(shape, 5)
+    inl, outl = inlet_tables(shape, 6)
+    geo = geo_mask(raw.astype(np.int32))
+    one = cases.mask_device(raw, inl, outl)
+    xa = x_align_for(geo, LBM_CASE_MASK)
+    slabs = []
+    for i in range(nslabs):
+        z0, z1 = cases.slab_bounds(nz, nslabs, i)
+        lat = cases.mask_device(cases.slab_mask(raw, z0, z1), inl, outl, z_offset=z0, nz_global=nz,
+                                halo_planes=True, x_align=xa)
+        assert np.array_equal(lat.geo(), geo[z0:z1]), f"slab {i} codes"
+        slabs.append((z0, z1, lat))
+    h1 = one.step(40)
+    hs = lbm_amd.group_step([s[2] for s in slabs], 40)
+    np.testing.assert_allclose(hs, h1, rtol=0, atol=1e-6)
+    ref = one.macros()
+    for z0, z1, lat in slabs:
+        for a, b in zip(lat.macros(), ref):
+            assert np.array_equal(a.view(np.uint32), b[z0:z1].view(np.uint32))

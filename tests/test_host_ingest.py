@@ -34,6 +34,20 @@ def test_bifurcation_mask_and_tables(lbm, oracle):
         assert n == n_o
         assert np.array_equal(inl.view(np.uint32), inl_o.view(np.uint32))
         assert np.array_equal(outl.view(np.uint32), outl_o.view(np.uint32))
+        # unmasked tables (device mask path): equal to the masked ones on the coded cells
+        n_u, inl_u, outl_u = lbm.read_bc_txt(os.path.join(BIF, "bc.txt"), geo.shape, block)
+        assert n_u == n
+        assert np.array_equal(np.where(geo[:, 1, :] == 2, inl_u, 0), inl)
+        assert np.array_equal(np.where(geo[:, -2, :] == 3, outl_u, 0), outl)
+
+
+def test_slab_mask_planes(lbm):
+    """slab_mask: the halo slab's raw planes z0-3 .. z1+2, zero outside the box."""
+    from lbm_amd import cases
+    raw = np.arange(5 * 6 * 7).reshape(5, 6, 7).astype(np.uint8)
+    m = cases.slab_mask(raw, 1, 3)
+    assert m.shape == (8, 6, 7)
+    assert not m[:2].any() and np.array_equal(m[2:7], raw) and not m[7].any()
 
 
 def test_known_answers(lbm):
