@@ -156,3 +156,22 @@ def bifurcation_device(inlet_block: int = 0, geo_path: str | None = None, bc_pat
     raw = read_geo_txt(geo_path, BIF_SHAPE)
     _, inl, outl = read_bc_txt(bc_path, tuple(BIF_SHAPE), inlet_block)
     return mask_device(raw.astype(np.uint8), inl, outl, device=device), raw
+
+
+def coronary_bc_codes(c_u: float = 2.74909090909091):
+    """The boundary codes of coronary.cu's boundary_stream (716-944) as LBM_CASE_GENERIC entries:
+    code 2 inlet (fluid at x+1): u_bc = (0.1745/C_U, 0, 0), rho_bc = 1;
+    code 3 outlet (fluid at x-1): u_bc = (0.1/C_U, 0, 0), rho of the fluid neighbour;
+    codes 5, 6, 7 outlets (fluid at z-1): u_bc = (0, 0, 0.02/C_U), rho of the fluid neighbour.
+    The velocities are the reference's double quotients rounded to float.  (The reference's
+    code-3 branch writes its q = 10 value into slot 14 with q = 9's operands -- a slip this
+    table does not copy: every outgoing q gets its own NEE value.)"""
+    from . import LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_FACE_NX, LBM_FACE_NZ, LBM_FACE_PX
+    cu = np.float32(c_u)
+    uin = float(np.float32(0.1745 / float(cu)))
+    uout = float(np.float32(0.1 / float(cu)))
+    uz = float(np.float32(0.02 / float(cu)))
+    codes = [{"code": 2, "face": LBM_FACE_PX, "kind": LBM_BC_VELOCITY_RHO, "rho": 1.0, "u": (uin, 0.0, 0.0)},
+             {"code": 3, "face": LBM_FACE_NX, "kind": LBM_BC_VELOCITY, "u": (uout, 0.0, 0.0)}]
+    codes += [{"code": k, "face": LBM_FACE_NZ, "kind": LBM_BC_VELOCITY, "u": (0.0, 0.0, uz)} for k in (5, 6, 7)]
+    return codes

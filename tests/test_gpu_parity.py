@@ -315,6 +315,29 @@ def test_generic_boundaries_bitwise(gpu, oracle, shape, cells_per_lane):
     assert o.bad_reads() == 0
 
 
+def test_coronary_codes_bitwise(gpu, oracle):
+    """coronary.cu's own code table (cases.coronary_bc_codes: 2 inlet +x with rho 1, 3 outlet
+    -x, 5/6/7 outlets -z) on a synthetic duct with three top-wall outlet patches."""
+    from lbm_amd import cases
+    nx, ny, nz = 30, 16, 14
+    geo, _, (rho, ux, uy, uz) = cases.duct_generic(nx, ny, nz)
+    geo[geo == 6] = 1
+    geo[geo == 5] = 1
+    for k, x0 in ((5, 5), (6, 12), (7, 20)):
+        geo[nz - 2, 6:9, x0:x0 + 3] = k
+    bcs = cases.coronary_bc_codes()
+    ux = np.where(geo == 2, np.float32(bcs[0]["u"][0]), np.where(geo == 3, np.float32(bcs[1]["u"][0]), 0))
+    uz = np.where((geo >= 5) & (geo <= 7), np.float32(bcs[2]["u"][2]), 0)
+    fields = (rho, ux.astype(np.float32), uy, uz.astype(np.float32))
+    lat = cases.generic(geo, bcs, fields, tau=0.6)
+    o = oracle.Oracle(oracle.GENERIC, geo, 0.6, bcs=bcs)
+    for s in (1, 60):
+        hg, ho = lat.step(s), o.step(s)
+        assert_bitwise(lat, o, geo, 2, f"coronary codes +{s}")
+        assert_residuals(hg, ho)
+    assert o.bad_reads() == 0
+
+
 @pytest.mark.parametrize("shape", [(37, 29, 23), (13, 11, 7), (66, 9, 31)])
 def test_ragged_shapes_bitwise(gpu, oracle, shape, cells_per_lane):
     """Extents that are not multiples of 4 (row padding, row shift, chunks straddling rows
