@@ -80,6 +80,7 @@ def small_case_mlups(n: int, steps: int, dev: int):
 
 
 def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
+    lay = lat.layout()
     lat.step(warm, history=False)
     lat.sync()
     t = time.perf_counter()
@@ -87,7 +88,10 @@ def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
     lat.sync()
     dt = time.perf_counter() - t
     lat.close()
-    return {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
+    out = {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
+    out["rows_along"] = "xy"[lay["row_axis"] - 1]
+    out["active_chunks"] = lay["active_chunks"]
+    return out
 
 
 def config_lines(dev: int):
@@ -98,6 +102,13 @@ def config_lines(dev: int):
     lat, geo = cases.poiseuille(128, 512, 128, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
     out["poiseuille_128x512x128 (C3)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
+    # the same lattice on the x-row layout (lbm_desc.row_axis = 1), for comparison
+    os.environ["LBM_ROW_AXIS"] = "x"
+    try:
+        lat, geo = cases.poiseuille(128, 512, 128, device=dev)
+    finally:
+        del os.environ["LBM_ROW_AXIS"]
+    out["poiseuille_128x512x128 (C3), x rows"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
     lat, geo, _, _ = cases.bifurcation(1, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
     out["bifurcation_64x83x32 (C4)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 2000)

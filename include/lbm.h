@@ -106,9 +106,10 @@ typedef struct {
   int device;              /* HIP device ordinal */
   int z_offset;            /* global z of local plane 0 */
   int nz_global;           /* global z extent (== nz for a single-domain run) */
-  /* Row alignment of the device layout: 1..4 = store cell x at slot x - (x_align - 1) of its
-   * row; 0 = choose it from geo so that most rows start their fluid run on a 4-cell boundary.
-   * Slabs of one lattice must use the same value (lbm_attach_rccl / lbm_group_step check). */
+  /* Row alignment of the device layout: 1..4 = store the cell at row position p (x, or y with
+   * row_axis 2) in slot p - (x_align - 1) of its row; 0 = choose it from geo so that most rows
+   * start their fluid run on a 4-cell boundary.  Slabs of one lattice must use the same value
+   * (lbm_attach_rccl / lbm_group_step check). */
   int x_align;
   /* LBM_CASE_GENERIC: the boundary codes (at most 16; copied at lbm_create). */
   const lbm_bc_code* bc_codes;
@@ -119,6 +120,12 @@ typedef struct {
    * nz + 6 with halo_planes = 1 (global z_offset-3 .. z_offset+nz+2; planes outside the global
    * box are never read).  Requires ny >= 5. */
   const uint8_t* mask;
+  /* Axis the device layout's rows (the contiguous, 4-cells-per-lane direction) run along:
+   * 1 = x, 2 = y, 0 = choose -- y when that leaves >= 3% fewer 256-cell chunks holding fluid
+   * (a pipe along y, Poiseulle.cu / bifurcation.cu, fills whole rows), x for the
+   * device-generated cavity and for slabs (nz_global != nz: give every slab the same value).
+   * Results are bit-identical for every choice; only addresses change. */
+  int row_axis;
 } lbm_desc;
 
 /* Status / version */
@@ -187,6 +194,10 @@ int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
  * the same step; retried_chunks counts those 256-cell chunks since creation.  Results are
  * bit-identical either way. */
 int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
+/* The device layout lbm_create chose (lbm_desc.row_axis / x_align resolved): row_axis 1 = x,
+ * 2 = y; pitch = row slots; x_align 1..4; active_chunks = 256-cell chunks k_step launches a
+ * wave for (those holding fluid).  Nullable outputs. */
+int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_t* active_chunks);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (done by the NEE blocks of
  * the step kernel). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);

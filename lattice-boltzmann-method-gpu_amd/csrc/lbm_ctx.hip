@@ -118,33 +118,85 @@ struct lbm_ctx {
 namespace {
 
 int64_t cell_of(const Layout& L, int x, int y, int z) {  // local z (storage plane z+1)
-  return (int64_t)(x - L.xshift) + (int64_t)y * L.pitch + (int64_t)(z + 1) * L.plane;
+  const int s0 = L.swap ? y : x, s1 = L.swap ? x : y;
+  return (int64_t)(s0 - L.xshift) + (int64_t)s1 * L.pitch + (int64_t)(z + 1) * L.plane;
 }
 
-// copy one raster row into storage, dropping the (outer, passive) cells the shift puts
-// before cell 0 (row 0 of storage plane 0 only)
+// copy one raster x-row (local plane z) into storage, dropping the (outer, passive) cells
+// the shift puts before cell 0 (row 0 of storage plane 0 only)
 template <class T>
-void put_row(std::vector<T>& h, int64_t at, const T* row, int nx) {
-  const int skip = at < 0 ? (int)-at : 0;
-  if (skip < nx) std::memcpy(&h[at + skip], row + skip, sizeof(T) * (nx - skip));
+void put_row(std::vector<T>& h, const Layout& L, int y, int z, const T* row) {
+  if (!L.swap) {
+    const int64_t at = cell_of(L, 0, y, z);
+    const int skip = at < 0 ? (int)-at : 0;
+    if (skip < L.nx) std::memcpy(&h[at + skip], row + skip, sizeof(T) * (L.nx - skip));
+    return;
+  }
+  for (int x = 0; x < L.nx; ++x) {
+    const int64_t at = cell_of(L, x, y, z);
+    if (at >= 0) h[at] = row[x];
+  }
 }
 
-// row shift that puts the most common first-fluid x of a row at a multiple of 4
-int choose_xshift(const lbm_desc& d) {
+// storage planes of the raster geo (nz, or nz + 2 with halo planes) and its fluid code
+int geo_planes(const lbm_desc& d) { return d.nz + (d.halo_planes ? 2 : 0); }
+int8_t fluid_code(const lbm_desc& d) { return d.case_kind == LBM_CASE_LDC ? 3 : 4; }
+
+// row shift that puts the most common first-fluid position of a storage row (along x, or
+// along y when swap) at a multiple of 4
+int choose_xshift(const lbm_desc& d, int swap) {
   if (d.x_align > 0) return d.x_align - 1;
   if (!d.geo) return 2;  // device-generated cavity: fluid starts at x = 2 (ldc.cu:469)
-  const int8_t fluid = d.case_kind == LBM_CASE_LDC ? 3 : 4;
-  const int rows = (d.nz + (d.halo_planes ? 2 : 0)) * d.ny;
+  const int8_t fluid = fluid_code(d);
+  const int n0 = swap ? d.ny : d.nx, n1 = swap ? d.nx : d.ny;
   int64_t hist[4] = {0, 0, 0, 0};
-  for (int r = 0; r < rows; ++r) {
-    const int8_t* row = d.geo + (int64_t)r * d.nx;
-    for (int x = 0; x < d.nx; ++x)
-      if (row[x] == fluid) {
-        hist[x & 3]++;
-        break;
+  for (int z = 0; z < geo_planes(d); ++z)
+    for (int s1 = 0; s1 < n1; ++s1)
+      for (int s0 = 0; s0 < n0; ++s0) {
+        const int x = swap ? s1 : s0, y = swap ? s0 : s1;
+        if (d.geo[((int64_t)z * d.ny + y) * d.nx + x] == fluid) {
+          hist[s0 & 3]++;
+          break;
+        }
       }
-  }
   return (int)(std::max_element(hist, hist + 4) - hist);
+}
+
+// 256-cell chunks holding a fluid cell (the waves k_step launches) when the rows run along
+// x (swap 0) or y (swap 1); fluid from the codes, or mask != 0 for a raw device mask
+int64_t active_chunks(const lbm_desc& d, int swap) {
+  const int n0 = swap ? d.ny : d.nx, n1 = swap ? d.nx : d.ny;
+  const int64_t pitch = (n0 + 3) / 4 * 4, plane = pitch * n1;
+  const int pad = d.geo ? (d.halo_planes ? 1 : 0) : (d.halo_planes ? 3 : 0);
+  const int8_t fluid = fluid_code(d);
+  std::vector<uint8_t> hit((size_t)((plane * (d.nz + 2) + 4) / kChunk + 2), 0);
+  for (int z = 0; z < d.nz; ++z)
+    for (int y = 0; y < d.ny; ++y)
+      for (int x = 0; x < d.nx; ++x) {
+        const int64_t r = ((int64_t)(z + pad) * d.ny + y) * d.nx + x;
+        if (d.geo ? d.geo[r] != fluid : d.mask[r] == 0) continue;
+        const int64_t c = (swap ? y : x) + (int64_t)(swap ? x : y) * pitch + (int64_t)(z + 1) * plane;
+        hit[c / kChunk] = 1;
+      }
+  int64_t n = 0;
+  for (uint8_t h : hit) n += h;
+  return n;
+}
+
+// lbm_desc.row_axis: 1 rows along x, 2 along y, 0 choose -- y when it leaves at least 3%
+// fewer active chunks (a pipe along y: whole fluid rows instead of partial x-rows);
+// slabs of a larger lattice and the device-generated cavity keep x unless told otherwise
+int choose_swap(const lbm_desc& d) {
+  int axis = d.row_axis;
+  if (axis == 0) {  // A/B and test switch: LBM_ROW_AXIS=x|y stands in for row_axis 0
+    const char* e = std::getenv("LBM_ROW_AXIS");
+    if (e && (e[0] == 'x' || e[0] == 'y')) axis = e[0] == 'x' ? 1 : 2;
+  }
+  if (axis == 1) return 0;
+  if (axis == 2) return 1;
+  if ((!d.geo && !d.mask) || (d.nz_global > 0 && d.nz_global != d.nz)) return 0;
+  const int64_t cx = active_chunks(d, 0), cy = active_chunks(d, 1);
+  return (double)cy < 0.97 * (double)cx ? 1 : 0;
 }
 
 // time one kernel launch with HIP events on its own stream (lbm_profile)
@@ -208,6 +260,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, b
   a.cells = r.cells; a.prev = r.prev; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
   a.nee_active = hstep == 0 ? 0 : 1;
   a.omc = c->omc;
+  a.swap = c->L.swap;
   if (out) *out = a;
   if (r.main_blocks + r.nee_blocks > 0) RCK(timed(c, st, 0, [&] { return launch_step(a, st); }));
   return LBM_OK;
@@ -297,7 +350,7 @@ int reset_state(lbm_ctx* c) {
     if (r->retry_cnt) HIPCK(c, hipMemset(r->retry_cnt, 0, sizeof(int)));
   }
   if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
-    HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->s_comp));
+    HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
     HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   c->steps_done = 0;
@@ -321,7 +374,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   *out = nullptr;
   const lbm_desc& d = *desc;
   if (d.nx < 3 || d.ny < 3 || d.nz < 1 || !(d.tau > 0.f) || d.case_kind < 0 || d.case_kind > 3 || d.x_align < 0 ||
-      d.x_align > 4 || d.n_bc_codes < 0 || d.n_bc_codes > kMaxBcCodes || (d.n_bc_codes > 0 && !d.bc_codes)) {
+      d.x_align > 4 || d.n_bc_codes < 0 || d.n_bc_codes > kMaxBcCodes || (d.n_bc_codes > 0 && !d.bc_codes) ||
+      d.row_axis < 0 || d.row_axis > 2) {
     g_create_error = "invalid lattice description";
     return LBM_ERR_ARG;
   }
@@ -360,10 +414,11 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
-  L.xshift = choose_xshift(d);
-  L.pitch = (d.nx + 3) / 4 * 4;
+  L.swap = choose_swap(c->d);
+  L.xshift = choose_xshift(d, L.swap);
+  L.pitch = ((L.swap ? d.ny : d.nx) + 3) / 4 * 4;
   L.planes = d.nz + 2;
-  L.plane = (int64_t)L.pitch * L.ny;
+  L.plane = (int64_t)L.pitch * (L.swap ? d.nx : d.ny);
   L.ncell = (L.plane * L.planes + kChunk - 1) / kChunk * kChunk;
   L.nchunk = L.ncell / kChunk;
   L.guard = (L.plane + L.pitch + 8 + kChunk - 1) / kChunk + 1;
@@ -441,26 +496,26 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       unsigned long long hh[4];
       CK(hipMalloc(&dh, sizeof(hh)));
       CK(hipMemsetAsync(dh, 0, sizeof(hh), c->s_comp));
-      CK(launch_mask_hist(dmask, d.nx, d.ny, c->d.nz_global, zbase, d.z_offset + lo, d.z_offset + hi, dh, c->s_comp));
+      CK(launch_mask_hist(dmask, d.nx, d.ny, c->d.nz_global, zbase, d.z_offset + lo, d.z_offset + hi, dh, L.swap,
+                          c->s_comp));
       CK(hipMemcpyAsync(hh, dh, sizeof(hh), hipMemcpyDeviceToHost, c->s_comp));
       CK(hipStreamSynchronize(c->s_comp));
       CK(hipFree(dh));
       L.xshift = (int)(std::max_element(hh, hh + 4) - hh);
     }
     CK(launch_mask_codes(dmask, d.nx, d.ny, c->d.nz_global, zbase, dcodes, L.pitch, L.xshift, L.plane, L.ncell,
-                         d.z_offset, lo, hi, c->s_comp));
+                         d.z_offset, lo, hi, L.swap, c->s_comp));
     CK(hipStreamSynchronize(c->s_comp));
     CK(hipFree(dmask));
   } else if (desc->geo) {
     std::vector<int8_t> h((size_t)L.ncell, 0);
     const int zlo = d.halo_planes ? -1 : 0, zhi = d.halo_planes ? d.nz + 1 : d.nz;
     for (int z = zlo; z < zhi; ++z)
-      for (int y = 0; y < d.ny; ++y)
-        put_row(h, cell_of(L, 0, y, z), desc->geo + ((int64_t)(z - zlo) * d.ny + y) * d.nx, d.nx);
+      for (int y = 0; y < d.ny; ++y) put_row(h, L, y, z, desc->geo + ((int64_t)(z - zlo) * d.ny + y) * d.nx);
     CK(hipMemcpyAsync(dcodes, h.data(), L.ncell, hipMemcpyHostToDevice, c->s_comp));
     CK(hipStreamSynchronize(c->s_comp));
   } else {
-    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.xshift, L.plane, L.ncell, d.z_offset, c->d.nz_global,
+    CK(launch_ldc_codes(dcodes, d.nx, d.ny, L.pitch, L.xshift, L.plane, L.ncell, d.z_offset, c->d.nz_global, L.swap,
                         c->s_comp));
   }
   const int64_t ntab = (int64_t)d.nx * c->d.nz_global;
@@ -501,6 +556,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   g.case_kind = d.case_kind; g.lid_u = d.lid_u;
   g.nx = d.nx; g.ny = d.ny; g.pitch = L.pitch; g.xshift = L.xshift; g.planes = L.planes; g.plane = L.plane; g.ncell = L.ncell;
   g.z_offset = d.z_offset; g.nz_global = c->d.nz_global;
+  g.swap = L.swap;
   CK(launch_classify(g, c->s_comp));
   CK(launch_flag_fluid(g, c->s_comp));
   CK(hipStreamSynchronize(c->s_comp));
@@ -581,8 +637,7 @@ int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux
     if (!host[k]) continue;
     h.assign((size_t)L.ncell, k == 0 ? 1.0f : 0.0f);
     for (int z = 0; z < L.nz; ++z)
-      for (int y = 0; y < L.ny; ++y)
-        std::memcpy(&h[cell_of(L, 0, y, z)], host[k] + ((int64_t)z * L.ny + y) * L.nx, sizeof(float) * L.nx);
+      for (int y = 0; y < L.ny; ++y) put_row(h, L, y, z, host[k] + ((int64_t)z * L.ny + y) * L.nx);
     HIPCK(c, hipMalloc(&dev[k], sizeof(float) * L.ncell));
     HIPCK(c, hipMemcpy(dev[k], h.data(), sizeof(float) * L.ncell, hipMemcpyHostToDevice));
   }
@@ -597,7 +652,8 @@ int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux
 int lbm_init_ldc(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
-  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.xshift, c->L.ny, c->d.lid_u, c->s_comp));
+  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.xshift, c->L.nx, c->L.ny, c->d.lid_u,
+                           c->L.swap, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -612,7 +668,7 @@ int lbm_init_case(lbm_ctx* c) {
   HIPCK(c, hipSetDevice(c->d.device));
   const Layout& L = c->L;
   HIPCK(c, launch_init_mask(c->buf[0], c->buf[1], c->codes, c->bc_in, c->bc_out, L.nx, L.ny, L.nz, L.pitch, L.xshift,
-                            L.plane, L.ncell, c->d.z_offset, c->s_comp));
+                            L.plane, L.ncell, c->d.z_offset, L.swap, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -876,6 +932,15 @@ int lbm_get_counts(lbm_ctx* c, int64_t* n_box, int64_t* n_fluid, double* algo_by
   return LBM_OK;
 }
 
+int lbm_get_layout(lbm_ctx* c, int* row_axis, int* pitch, int* x_align, int64_t* active_chunks) {
+  if (!c) return LBM_ERR_ARG;
+  if (row_axis) *row_axis = c->L.swap ? 2 : 1;
+  if (pitch) *pitch = c->L.pitch;
+  if (x_align) *x_align = c->L.xshift + 1;
+  if (active_chunks) *active_chunks = c->whole.nchunks;
+  return LBM_OK;
+}
+
 int lbm_get_boundary_cells(lbm_ctx* c, int64_t* n_boundary) {
   if (!c || !n_boundary) return LBM_ERR_ARG;
   *n_boundary = c->n_slow;
@@ -932,7 +997,8 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
   c->rank = rank;
   c->nranks = nranks;
   {  // every slab must use the same row layout: the halo planes are copied cell for cell
-    int h[2] = {c->L.pitch * 4 + c->L.xshift, -(c->L.pitch * 4 + c->L.xshift)};
+    const int key = (c->L.pitch * 4 + c->L.xshift) * 2 + c->L.swap;
+    int h[2] = {key, -key};
     int* dv = nullptr;
     HIPCK(c, hipMalloc(&dv, sizeof(h)));
     HIPCK(c, hipMemcpy(dv, h, sizeof(h), hipMemcpyHostToDevice));
@@ -941,7 +1007,8 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
     HIPCK(c, hipMemcpy(h, dv, sizeof(h), hipMemcpyDeviceToHost));
     HIPCK(c, hipFree(dv));
     if (h[0] != -h[1]) {
-      c->err = "slabs differ in row layout (pitch / x alignment); give every rank the same nx and fluid x range";
+      c->err = "slabs differ in row layout (row axis / pitch / alignment); give every rank the same nx, ny, "
+               "row_axis and x_align";
       return LBM_ERR_GEOMETRY;
     }
   }
@@ -978,7 +1045,8 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   if (!cs || n < 1 || nsteps < 0) return LBM_ERR_ARG;
   lbm_ctx* c0 = cs[0];
   for (int i = 0; i < n; ++i) {
-    if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xshift != c0->L.xshift || cs[i]->L.ny != c0->L.ny ||
+    if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xshift != c0->L.xshift ||
+        cs[i]->L.swap != c0->L.swap || cs[i]->L.plane != c0->L.plane ||
         cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled || cs[i]->comm) {
       c0->err = "lbm_group_step: slabs must share device, row layout (nx, ny, x_align) and step count, "
                 "without convergence control or RCCL";

@@ -63,9 +63,24 @@ __device__ __forceinline__ float lane_from_next(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
-template <int Q>
+// Storage direction of population Q.  The layout's rows run along physical x, or along y
+// when SW (lbm_desc.row_axis: a pipe along y then fills whole rows); z is always the slab
+// axis.  Only addresses change with SW -- the arithmetic stays in physical q order.
+template <int Q, bool SW>
+struct SDir {
+  static constexpr int x = SW ? Dir<Q>::y : Dir<Q>::x;  // along the row: +-1 cell
+  static constexpr int y = SW ? Dir<Q>::x : Dir<Q>::y;  // across rows: +-pitch
+  static constexpr int z = Dir<Q>::z;                   // across planes: +-plane
+};
+
+template <int Q, bool SW>
 constexpr int64_t row_off(int pitch, int64_t plane) {
-  return Dir<Q>::y * (int64_t)pitch + Dir<Q>::z * plane;
+  return SDir<Q, SW>::y * (int64_t)pitch + SDir<Q, SW>::z * plane;
+}
+// storage offset of e_Q: population Q of cell c is pulled from c - cell_off
+template <int Q, bool SW>
+constexpr int64_t cell_off(int pitch, int64_t plane) {
+  return SDir<Q, SW>::x + row_off<Q, SW>(pitch, plane);
 }
 
 // Pull of population Q for the lane's 4 cells c..c+3 from c - e_Q .. c+3 - e_Q, in two
@@ -75,22 +90,22 @@ constexpr int64_t row_off(int pitch, int64_t plane) {
 //           address (chunk base cb), so a scalar load with no branch;
 //  compose: shift the slice by one cell across lanes (DPP) and drop the edge float into
 //           lane 0 (e_x = +1) or lane 63 (e_x = -1).
-template <int Q>
+template <int Q, bool SW>
 __device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t cb, int64_t c,
                                            int pitch, int64_t plane) {
-  const int64_t ro = row_off<Q>(pitch, plane);
+  const int64_t ro = row_off<Q, SW>(pitch, plane);
   // non-temporal: every slice is read once per step (no measurable change against plain
   // loads in interleaved A/B runs; the lines two chunks share still meet in the XCD's L2)
   a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + aidx(c - ro, Q)));
-  if constexpr (Dir<Q>::x == 1) e = src[aidx(cb - ro - 1, Q)];                  // lane 0: b - 1
-  else if constexpr (Dir<Q>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];       // lane 63: b + 4
+  if constexpr (SDir<Q, SW>::x == 1) e = src[aidx(cb - ro - 1, Q)];             // lane 0: b - 1
+  else if constexpr (SDir<Q, SW>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];  // lane 63: b + 4
 }
 
-template <int Q>
+template <int Q, bool SW>
 __device__ __forceinline__ f4 pull_compose(const f4 a, float e, int lane) {
-  if constexpr (Dir<Q>::x == 0) {
+  if constexpr (SDir<Q, SW>::x == 0) {
     return a;
-  } else if constexpr (Dir<Q>::x == 1) {  // needs b-1 .. b+2
+  } else if constexpr (SDir<Q, SW>::x == 1) {  // needs b-1 .. b+2
     const float p = lane_from_prev(a.w);
     return f4{lane == 0 ? e : p, a.x, a.y, a.z};
   } else {                                 // needs b+1 .. b+4
@@ -99,12 +114,12 @@ __device__ __forceinline__ f4 pull_compose(const f4 a, float e, int lane) {
   }
 }
 
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t cb, int64_t c, int lane,
                                           int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
   float e[kQ];
-  ((pull_issue<Qs>(v[Qs], e[Qs], src, cb, c, pitch, plane)), ...);
-  ((v[Qs] = pull_compose<Qs>(v[Qs], e[Qs], lane)), ...);
+  ((pull_issue<Qs, SW>(v[Qs], e[Qs], src, cb, c, pitch, plane)), ...);
+  ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], lane)), ...);
 }
 
 template <int J, int... Qs>
@@ -120,19 +135,19 @@ using AllQ = std::make_integer_sequence<int, kQ>;
 // pulls at the next step -- exactly the value boundary_stream writes there
 // (Poiseulle.cu:601-746: d_dst[q][W] = d_dst[opp q][W + e_q]).  Each wall slot has one
 // writer (W + e_q), the consumer, so the slot always lives in the writer's own storage.
-template <int Q>
+template <int Q, bool SW>
 __device__ __forceinline__ void bb_store_one(float* __restrict__ dst, int64_t c, uint32_t m, float out_opp,
                                              int pitch, int64_t plane) {
   if constexpr (Q > 0) {
-    if (m & (1u << Q)) dst[aidx(c - (Dir<Q>::x + row_off<Q>(pitch, plane)), Q)] = out_opp;
+    if (m & (1u << Q)) dst[aidx(c - cell_off<Q, SW>(pitch, plane), Q)] = out_opp;
   }
 }
 // one set bit at a time (rare path: keeps the address arithmetic out of the hot registers)
-template <int J>
+template <int J, bool SW>
 __device__ __forceinline__ void bb_store_cell(float* __restrict__ dst, int64_t c, uint32_t m, const f4* v, int pitch,
                                               int64_t plane) {
 #define LBM_BB_CASE(Q) \
-  case Q: dst[aidx(c + J - (Dir<Q>::x + row_off<Q>(pitch, plane)), Q)] = v[Dir<Q>::opp][J]; break;
+  case Q: dst[aidx(c + J - cell_off<Q, SW>(pitch, plane), Q)] = v[Dir<Q>::opp][J]; break;
   // opaque copy of c: otherwise the compiler CSEs these offsets with the pull addresses of
   // the same directions and keeps ~70 VGPRs of them alive across the collision (240 vs 167)
   asm volatile("" : "+v"(c));
@@ -199,12 +214,12 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain; a wave that does not
 //        stores nothing and queues its chunk for the exact path, run by the reduction
 //        launch (both paths in one kernel would cost a third of the registers: 232 vs 168).
-template <bool FAST>
+template <bool FAST, bool SW>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane) {
   double acc = 0.0;
   const int64_t c = cb + lane * 4;
   f4 v[kQ];
-  pull4_all(v, a.src, cb, c, lane, a.pitch, a.plane, AllQ{});
+  pull4_all<SW>(v, a.src, cb, c, lane, a.pitch, a.plane, AllQ{});
   const unsigned t4 = *reinterpret_cast<const unsigned*>(a.type + c);
   // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
   // so this dependent load hides behind the arithmetic)
@@ -276,10 +291,10 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   relax_cell<2, FAST>(v, a.tau, a.tau_rcp, r2, x2, y2, z2, AllQ{});
   relax_cell<3, FAST>(v, a.tau, a.tau_rcp, r3, x3, y3, z3, AllQ{});
   if (t4 & kWall4) {  // rare, divergent: lanes holding wall-adjacent cells
-    if (store & 1u) bb_store_cell<0>(a.dst, c, m0, v, a.pitch, a.plane);
-    if (store & 2u) bb_store_cell<1>(a.dst, c, m1, v, a.pitch, a.plane);
-    if (store & 4u) bb_store_cell<2>(a.dst, c, m2, v, a.pitch, a.plane);
-    if (store & 8u) bb_store_cell<3>(a.dst, c, m3, v, a.pitch, a.plane);
+    if (store & 1u) bb_store_cell<0, SW>(a.dst, c, m0, v, a.pitch, a.plane);
+    if (store & 2u) bb_store_cell<1, SW>(a.dst, c, m1, v, a.pitch, a.plane);
+    if (store & 4u) bb_store_cell<2, SW>(a.dst, c, m2, v, a.pitch, a.plane);
+    if (store & 8u) bb_store_cell<3, SW>(a.dst, c, m3, v, a.pitch, a.plane);
   }
   float* d = a.dst + aidx(c, 0);
   if (whole) {
@@ -302,9 +317,9 @@ struct Macro {
   float rho, ux, uy, uz;
 };
 
-template <int Q>
+template <int Q, bool SW>
 __device__ __forceinline__ void fix_pull(float* f, const MainArgs& a, int64_t c, const Macro& mp) {
-  const int64_t nb = c - (Dir<Q>::x + row_off<Q>(a.pitch, a.plane));
+  const int64_t nb = c - cell_off<Q, SW>(a.pitch, a.plane);
   f[Q] = a.src[aidx(nb, Q)];
   if constexpr (Q == 0) return;
   const uint8_t tn = a.type[nb];
@@ -328,10 +343,10 @@ __device__ __forceinline__ void fix_pull(float* f, const MainArgs& a, int64_t c,
   }
 }
 
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ void fix_pull_all(float* f, const MainArgs& a, int64_t c, const Macro& mp,
                                              std::integer_sequence<int, Qs...>) {
-  (fix_pull<Qs>(f, a, c, mp), ...);
+  (fix_pull<Qs, SW>(f, a, c, mp), ...);
 }
 
 template <int... Qs>
@@ -339,23 +354,24 @@ __device__ __forceinline__ void fix_relax_all(float* f, float tau, float r, floa
                                               std::integer_sequence<int, Qs...>) {
   ((f[Qs] = f[Qs] - (f[Qs] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
 }
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m,
                                               int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
   ((dst[aidx(c, Qs)] = f[Qs]), ...);
-  if (m) (bb_store_one<Qs>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
+  if (m) (bb_store_one<Qs, SW>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
 }
 
 // One NEE-adjacent fluid cell (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021
 // applied on the consumer side): its pulls with the NEE value substituted for every
 // population an NEE neighbour supplies, collide (exact division), store incl. its own
 // bounce-back slots, keep its (rho, u) for the next step's NEE values.
+template <bool SW>
 __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const int64_t c = a.cells[i];
   const float4 pv = a.prev[i];
   const Macro mp{pv.x, pv.y, pv.z, pv.w};
   float f[kQ];
-  fix_pull_all(f, a, c, mp, AllQ{});
+  fix_pull_all<SW>(f, a, c, mp, AllQ{});
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
@@ -363,7 +379,7 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
-  fix_store_all(f, a.dst, c, a.links[c], a.pitch, a.plane, AllQ{});
+  fix_store_all<SW>(f, a.dst, c, a.links[c], a.pitch, a.plane, AllQ{});
   a.prev[i] = make_float4(rho, ux, uy, uz);
   if (a.store_all_macros) {
     a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
@@ -373,19 +389,20 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
 
 // One cell per lane (small lattices: a wave per 64 cells, so 4x the waves of the chunk path
 // and a quarter of its per-wave latency): plain pulls, exact division, bounce-back slots.
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ void pull1_all(float* f, const float* __restrict__ src, int64_t c, int pitch,
                                           int64_t plane, std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = __builtin_nontemporal_load(src + aidx(c - (Dir<Qs>::x + row_off<Qs>(pitch, plane)), Qs))), ...);
+  ((f[Qs] = __builtin_nontemporal_load(src + aidx(c - cell_off<Qs, SW>(pitch, plane), Qs))), ...);
 }
 
+template <bool SW>
 __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
   const uint8_t t = a.type[c];
   const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid &&
                   !(t & kNeedsMac);
   if (!in) return 0.0;
   float f[kQ];
-  pull1_all(f, a.src, c, a.pitch, a.plane, AllQ{});
+  pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
@@ -393,7 +410,7 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
-  fix_store_all(f, a.dst, c, (t & kWallAdj) ? a.links[c] : 0u, a.pitch, a.plane, AllQ{});
+  fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? a.links[c] : 0u, a.pitch, a.plane, AllQ{});
   if (a.store_all_macros) {
     a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
   }
@@ -402,7 +419,7 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
 
 // ---- the step kernel -------------------------------------------------------------------
 
-template <bool FAST, bool QUARTER>
+template <bool FAST, bool QUARTER, bool SW>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -419,15 +436,15 @@ __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
     const int idx = slot * (kBlock / 64) + wave;
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
-        acc = process_cell1(a, (int64_t)a.chunks[idx >> 2] * kChunk + (idx & 3) * 64 + lane);
+        acc = process_cell1<SW>(a, (int64_t)a.chunks[idx >> 2] * kChunk + (idx & 3) * 64 + lane);
     } else if (idx < a.nchunks) {
-      acc = process_chunk<FAST>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
+      acc = process_chunk<FAST, SW>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
     }
     slot += a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
     slot = blockIdx.x;
     const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
-    if (i < a.n_nee) acc = nee_cell(a, i);
+    if (i < a.n_nee) acc = nee_cell<SW>(a, i);
   }
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[slot] = s;
@@ -466,7 +483,8 @@ __global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict_
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int k = (int)blockIdx.x * 4 + wave; k < nq; k += (int)gridDim.x * 4)
-      r += process_chunk<false>(m, (int64_t)m.retry[k] * kChunk, lane);
+      r += m.swap ? process_chunk<false, true>(m, (int64_t)m.retry[k] * kChunk, lane)
+                  : process_chunk<false, false>(m, (int64_t)m.retry[k] * kChunk, lane);
   }
   __syncthreads();  // red[] reuse
   r = block_sum(r, red);
@@ -513,7 +531,8 @@ __global__ __launch_bounds__(512) void k_reduce_one(const double* __restrict__ p
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int k = wave; k < nq; k += (int)(blockDim.x >> 6))
-      r += process_chunk<false>(m, (int64_t)m.retry[k] * kChunk, lane);
+      r += m.swap ? process_chunk<false, true>(m, (int64_t)m.retry[k] * kChunk, lane)
+                  : process_chunk<false, false>(m, (int64_t)m.retry[k] * kChunk, lane);
   }
   __syncthreads();  // red[] reuse
   r = block_sum(r, red);
@@ -561,35 +580,54 @@ __global__ void k_unpack(float* __restrict__ f, const float* __restrict__ buf, c
 
 // LDC bounce-back already at step 0 (ldc.cu:75-202 swaps in place before the fluid reads):
 // seed the wall slots of buffer f from the initial populations, as the producers would have
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ void prime_cell(float* f, int64_t c, uint32_t m, int pitch, int64_t plane,
                                            std::integer_sequence<int, Qs...>) {
-  (bb_store_one<Qs>(f, c, m, f[aidx(c, Dir<Qs>::opp)], pitch, plane), ...);
+  (bb_store_one<Qs, SW>(f, c, m, f[aidx(c, Dir<Qs>::opp)], pitch, plane), ...);
 }
+template <bool SW>
 __global__ void k_bb_prime(float* f, const uint8_t* __restrict__ type, const uint32_t* __restrict__ links,
                            int64_t ncell, int pitch, int64_t plane) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * blockDim.x) {
     const uint8_t t = type[c];
     if ((t & kClassMask) != kFluid || !(t & kWallAdj)) continue;
-    prime_cell(f, c, links[c], pitch, plane, AllQ{});
+    prime_cell<SW>(f, c, links[c], pitch, plane, AllQ{});
   }
 }
 
 // ---- geometry --------------------------------------------------------------------------
+
+// storage cell -> physical (x, y, storage plane zs): c + shift = s0 + s1*pitch + zs*plane with
+// (s0, s1) = (x, y), or (y, x) when the rows run along y; in = inside the box's rows
+struct CellPos {
+  int x, y, zs;
+  bool in;
+};
+__device__ __forceinline__ CellPos cell_pos(int64_t c, int shift, int pitch, int64_t plane, int nx, int ny, int swap) {
+  const int64_t u = c + shift;
+  const int s0 = (int)(u % pitch);
+  const int n1 = swap ? nx : ny;
+  const int s1 = (int)((u / pitch) % n1);
+  CellPos p;
+  p.zs = (int)(u / plane);
+  p.x = swap ? s1 : s0;
+  p.y = swap ? s0 : s1;
+  p.in = s0 < (swap ? ny : nx);
+  return p;
+}
 
 // reference code -> class/face/kind; NEE data into the macro arrays of NEE cells
 __global__ void k_classify(const GeoArgs g) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
     const int code = g.codes[c];
-    const int64_t u = c + g.xshift;  // unshifted index x + y*pitch + zs*plane
-    const int x = (int)(u % g.pitch);
-    const int zs = (int)(u / g.plane);
+    const CellPos p = cell_pos(c, g.xshift, g.pitch, g.plane, g.nx, g.ny, g.swap);
+    const int x = p.x, zs = p.zs;
     const int zg = zs - 1 + g.z_offset;  // global z
     uint8_t t = kPassive;
     const float kRhoOfFluid = __builtin_nanf("");  // rho slot of a velocity NEE cell: use rho_F
-    if (x < g.nx && zs < g.planes) {
-      const int y = (int)((u / g.pitch) % g.ny);
+    if (p.in && zs < g.planes) {
+      const int y = p.y;
       if (g.case_kind == 0) {  // LDC (ldc.cu:469): 0 ghost, 1 wall, 2 lid, 3 fluid
         if (code == 1) t = kWall;
         else if (code == 3) t = kFluid;
@@ -641,10 +679,10 @@ __global__ void k_classify(const GeoArgs g) {
   }
 }
 
-template <int Q>
+template <int Q, bool SW>
 __device__ __forceinline__ void scan_nb(const uint8_t* type, int64_t c, const GeoArgs& g, uint8_t& flags,
                                         uint32_t& walls) {
-  const int64_t nb = c - (Dir<Q>::x + Dir<Q>::y * (int64_t)g.pitch + Dir<Q>::z * g.plane);
+  const int64_t nb = c - cell_off<Q, SW>(g.pitch, g.plane);
   if (Q == 0 || nb < 0 || nb >= g.ncell) return;
   const uint8_t tn = type[nb];
   const int cls = tn & kClassMask;
@@ -655,12 +693,13 @@ __device__ __forceinline__ void scan_nb(const uint8_t* type, int64_t c, const Ge
   if (cls == kNee && ((face_bits<Q>() >> nee_face(tn)) & 1)) flags |= kNeedsMac;
 }
 
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ void scan_all(const uint8_t* type, int64_t c, const GeoArgs& g, uint8_t& flags,
                                          uint32_t& walls, std::integer_sequence<int, Qs...>) {
-  (scan_nb<Qs>(type, c, g, flags, walls), ...);
+  (scan_nb<Qs, SW>(type, c, g, flags, walls), ...);
 }
 
+template <bool SW>
 __global__ void k_flag_fluid(const GeoArgs g) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
@@ -668,7 +707,7 @@ __global__ void k_flag_fluid(const GeoArgs g) {
     if ((t & kClassMask) != kFluid) continue;
     uint8_t flags = 0;
     uint32_t walls = 0;
-    scan_all(g.type, c, g, flags, walls, AllQ{});
+    scan_all<SW>(g.type, c, g, flags, walls, AllQ{});
     g.type[c] = (uint8_t)(t | flags);
     g.links[c] = walls;
   }
@@ -676,31 +715,31 @@ __global__ void k_flag_fluid(const GeoArgs g) {
 
 // passive cells some fluid cell pulls from (malformed geometry, the reference reads their
 // initial values forever): flag them so the main kernel never overwrites them
-template <int... Qs>
+template <bool SW, int... Qs>
 __device__ __forceinline__ bool pulled_by_fluid(const uint8_t* type, int64_t c, const GeoArgs& g,
                                                 std::integer_sequence<int, Qs...>) {
   auto fl = [&](int64_t n) { return n >= 0 && n < g.ncell && (type[n] & kClassMask) == kFluid; };
-  return (fl(c + Dir<Qs>::x + Dir<Qs>::y * (int64_t)g.pitch + Dir<Qs>::z * g.plane) || ...);
+  return (fl(c + cell_off<Qs, SW>(g.pitch, g.plane)) || ...);
 }
 
+template <bool SW>
 __global__ void k_mark_pulled(const GeoArgs g) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
     const uint8_t t = g.type[c];
-    if ((t & kClassMask) == kPassive && pulled_by_fluid(g.type, c, g, AllQ{})) g.type[c] = (uint8_t)(t | kPulled);
+    if ((t & kClassMask) == kPassive && pulled_by_fluid<SW>(g.type, c, g, AllQ{})) g.type[c] = (uint8_t)(t | kPulled);
   }
 }
 
 __global__ void k_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift, int64_t plane, int64_t ncell,
-                            int z_offset, int nzg) {
+                            int z_offset, int nzg, int swap) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t u = c + xshift;
-    const int x = (int)(u % pitch);
-    const int y = (int)((u / pitch) % ny);
-    const int z = (int)(u / plane) - 1 + z_offset;
+    const CellPos p = cell_pos(c, xshift, pitch, plane, nx, ny, swap);
+    const int x = p.x, y = p.y;
+    const int z = p.zs - 1 + z_offset;
     int8_t code = 0;  // ldc.cu:468-502
-    if (x < nx && z >= 0 && z < nzg) {
+    if (p.in && z >= 0 && z < nzg) {
       if (x >= 1 && x < nx - 1 && y >= 1 && y < ny - 1 && z >= 1 && z < nzg - 1) code = 1;
       if (x >= 2 && x < nx - 2 && y >= 2 && y < ny - 2 && z >= 2 && z < nzg - 2) code = 3;
       if (y == ny - 2 && x >= 1 && x < nx - 1 && z >= 1 && z < nzg - 1) code = 2;
@@ -758,15 +797,17 @@ __device__ int mask_code(const MaskGeo& g, int x, int y, int z) {
   return 0;
 }
 
-// first fluid (code 4) x of every row of planes z_lo .. z_hi-1 -> hist[x & 3] (choose_xshift)
-__global__ void k_mask_hist(MaskGeo g, int z_lo, int z_hi, unsigned long long* hist) {
-  const int64_t rows = (int64_t)(z_hi - z_lo) * g.ny;
+// first fluid (code 4) position along every storage row (x rows, or y rows when swap) of
+// planes z_lo .. z_hi-1 -> hist[pos & 3] (choose_xshift)
+__global__ void k_mask_hist(MaskGeo g, int z_lo, int z_hi, unsigned long long* hist, int swap) {
+  const int n0 = swap ? g.ny : g.nx, n1 = swap ? g.nx : g.ny;
+  const int64_t rows = (int64_t)(z_hi - z_lo) * n1;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
-    const int y = (int)(r % g.ny), z = z_lo + (int)(r / g.ny);
+    const int s1 = (int)(r % n1), z = z_lo + (int)(r / n1);
     if (z < 0 || z >= g.nzg) continue;
-    for (int x = 0; x < g.nx; ++x)
-      if (mask_code(g, x, y, z) == 4) {
-        atomicAdd(&hist[x & 3], 1ull);
+    for (int s0 = 0; s0 < n0; ++s0)
+      if (mask_code(g, swap ? s1 : s0, swap ? s0 : s1, z) == 4) {
+        atomicAdd(&hist[s0 & 3], 1ull);
         break;
       }
   }
@@ -775,16 +816,14 @@ __global__ void k_mask_hist(MaskGeo g, int z_lo, int z_hi, unsigned long long* h
 // codes of every storage cell (layout order, as k_ldc_codes); storage planes outside
 // z_lo .. z_hi-1 (local) or outside the global box stay 0
 __global__ void k_mask_codes(MaskGeo g, int8_t* codes, int pitch, int xshift, int64_t plane, int64_t ncell,
-                             int z_offset, int z_lo, int z_hi) {
+                             int z_offset, int z_lo, int z_hi, int swap) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t u = c + xshift;
-    const int x = (int)(u % pitch);
-    const int y = (int)((u / pitch) % g.ny);
-    const int zl = (int)(u / plane) - 1;
+    const CellPos p = cell_pos(c, xshift, pitch, plane, g.nx, g.ny, swap);
+    const int zl = p.zs - 1;
     const int z = zl + z_offset;
     int8_t code = 0;
-    if (x < g.nx && zl >= z_lo && zl < z_hi && z >= 0 && z < g.nzg) code = (int8_t)mask_code(g, x, y, z);
+    if (p.in && zl >= z_lo && zl < z_hi && z >= 0 && z < g.nzg) code = (int8_t)mask_code(g, p.x, p.y, z);
     codes[c] = code;
   }
 }
@@ -795,15 +834,15 @@ __global__ void k_mask_codes(MaskGeo g, int8_t* codes, int pitch, int xshift, in
 // y = 1) and outlet (code 3, row y = ny-2) cells of the local planes, from the bc tables
 // (x + global z * nx); expanded equilibrium into both buffers
 __global__ void k_init_mask(float* fa, float* fb, const int8_t* codes, const float* in_uy, const float* out_uy, int nx,
-                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset) {
+                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
+                            int swap) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t u = c + xshift;
-    const int x = (int)(u % pitch);
-    const int y = (int)((u / pitch) % ny);
-    const int zl = (int)(u / plane) - 1;
+    const CellPos p = cell_pos(c, xshift, pitch, plane, nx, ny, swap);
+    const int x = p.x, y = p.y;
+    const int zl = p.zs - 1;
     float vy = 0.0f;
-    if (x < nx && zl >= 0 && zl < nz) {
+    if (p.in && zl >= 0 && zl < nz) {
       const int64_t t = x + (int64_t)(zl + z_offset) * nx;
       if (y == 1 && codes[c] == 2 && in_uy) vy = in_uy[t];
       if (y == ny - 2 && codes[c] == 3 && out_uy) vy = out_uy[t];
@@ -828,9 +867,10 @@ __global__ void k_init_feq(float* fa, float* fb, int64_t n, int form, const floa
   }
 }
 
-__global__ void k_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int ny, float lid_u) {
+__global__ void k_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int nx, int ny, float lid_u,
+                           int swap) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
-    const int y = (int)(((c + xshift) / pitch) % ny);
+    const int y = cell_pos(c, xshift, pitch, (int64_t)pitch * (swap ? nx : ny), nx, ny, swap).y;
     // ldc.cu:510-532: rho 1, u 0; uz = u_max on y = ny-1 and y = ny-2
     const float uz = (y == ny - 1 || y == ny - 2) ? lid_u : 0.0f;
     float e[kQ];
@@ -879,12 +919,19 @@ constexpr size_t kOccupancyLds = 56 * 1024;
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   const dim3 grid(a.main_blocks + a.nee_blocks);
-  if (a.quarter)  // latency-bound sizes: as many resident waves as the registers allow
-    hipLaunchKernelGGL((k_step<false, true>), grid, dim3(kBlock), 0, s, a);
-  else if (a.fast_div)
-    hipLaunchKernelGGL((k_step<true, false>), grid, dim3(kBlock), kOccupancyLds, s, a);
-  else
-    hipLaunchKernelGGL((k_step<false, false>), grid, dim3(kBlock), kOccupancyLds, s, a);
+  typedef void (*Kern)(const MainArgs);
+  const bool sw = a.swap != 0;
+  Kern k;
+  size_t lds = kOccupancyLds;
+  if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
+    k = sw ? k_step<false, true, true> : k_step<false, true, false>;
+    lds = 0;
+  } else if (a.fast_div) {
+    k = sw ? k_step<true, false, true> : k_step<true, false, false>;
+  } else {
+    k = sw ? k_step<false, false, true> : k_step<false, false, false>;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, a);
   return hipGetLastError();
 }
 
@@ -923,8 +970,9 @@ hipError_t launch_unpack(float* f, const float* buf, const uint8_t* type, int zs
 }
 
 hipError_t launch_bb_prime(float* f, const uint8_t* type, const uint32_t* links, int64_t ncell, int pitch, int64_t plane,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(k_bb_prime, dim3(grid_for(ncell, 256)), dim3(256), 0, s, f, type, links, ncell, pitch, plane);
+                           int swap, hipStream_t s) {
+  hipLaunchKernelGGL(swap ? k_bb_prime<true> : k_bb_prime<false>, dim3(grid_for(ncell, 256)), dim3(256), 0, s, f, type,
+                     links, ncell, pitch, plane);
   return hipGetLastError();
 }
 
@@ -934,32 +982,34 @@ hipError_t launch_classify(const GeoArgs& g, hipStream_t s) {
 }
 
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_flag_fluid, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s, g);
-  hipLaunchKernelGGL(k_mark_pulled, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(g.swap ? k_flag_fluid<true> : k_flag_fluid<false>, dim3(grid_for(g.ncell, 256)), dim3(256), 0, s,
+                     g);
+  hipLaunchKernelGGL(g.swap ? k_mark_pulled<true> : k_mark_pulled<false>, dim3(grid_for(g.ncell, 256)), dim3(256), 0,
+                     s, g);
   return hipGetLastError();
 }
 
 hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift, int64_t plane, int64_t ncell,
-                            int z_offset, int nz_global, hipStream_t s) {
+                            int z_offset, int nz_global, int swap, hipStream_t s) {
   hipLaunchKernelGGL(k_ldc_codes, dim3(grid_for(ncell, 256)), dim3(256), 0, s, codes, nx, ny, pitch, xshift, plane,
-                     ncell, z_offset, nz_global);
+                     ncell, z_offset, nz_global, swap);
   return hipGetLastError();
 }
 
 hipError_t launch_mask_hist(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int z_lo, int z_hi,
-                            unsigned long long* hist, hipStream_t s) {
+                            unsigned long long* hist, int swap, hipStream_t s) {
   const MaskGeo g{mask, nx, ny, nz_global, zbase};
-  hipLaunchKernelGGL(k_mask_hist, dim3(grid_for((int64_t)(z_hi - z_lo) * ny, 256)), dim3(256), 0, s, g, z_lo, z_hi,
-                     hist);
+  hipLaunchKernelGGL(k_mask_hist, dim3(grid_for((int64_t)(z_hi - z_lo) * (swap ? nx : ny), 256)), dim3(256), 0, s, g,
+                     z_lo, z_hi, hist, swap);
   return hipGetLastError();
 }
 
 hipError_t launch_mask_codes(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int8_t* codes, int pitch,
-                             int xshift, int64_t plane, int64_t ncell, int z_offset, int z_lo, int z_hi,
+                             int xshift, int64_t plane, int64_t ncell, int z_offset, int z_lo, int z_hi, int swap,
                              hipStream_t s) {
   const MaskGeo g{mask, nx, ny, nz_global, zbase};
   hipLaunchKernelGGL(k_mask_codes, dim3(grid_for(ncell, 256)), dim3(256), 0, s, g, codes, pitch, xshift, plane, ncell,
-                     z_offset, z_lo, z_hi);
+                     z_offset, z_lo, z_hi, swap);
   return hipGetLastError();
 }
 
@@ -970,15 +1020,16 @@ hipError_t launch_init_feq(float* fa, float* fb, int64_t n, int form, const floa
 }
 
 hipError_t launch_init_mask(float* fa, float* fb, const int8_t* codes, const float* in_uy, const float* out_uy, int nx,
-                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
+                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset, int swap,
                             hipStream_t s) {
   hipLaunchKernelGGL(k_init_mask, dim3(grid_for(ncell, 256)), dim3(256), 0, s, fa, fb, codes, in_uy, out_uy, nx, ny, nz,
-                     pitch, xshift, plane, ncell, z_offset);
+                     pitch, xshift, plane, ncell, z_offset, swap);
   return hipGetLastError();
 }
 
-hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int ny, float lid_u, hipStream_t s) {
-  hipLaunchKernelGGL(k_init_ldc, dim3(grid_for(n, 256)), dim3(256), 0, s, fa, fb, n, pitch, xshift, ny, lid_u);
+hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int nx, int ny, float lid_u, int swap,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_init_ldc, dim3(grid_for(n, 256)), dim3(256), 0, s, fa, fb, n, pitch, xshift, nx, ny, lid_u, swap);
   return hipGetLastError();
 }
 

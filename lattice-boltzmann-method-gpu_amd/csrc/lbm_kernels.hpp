@@ -35,6 +35,9 @@ struct Layout {
   int64_t ncell;      // plane * planes rounded up to a whole chunk
   int64_t nchunk;     // ncell / 256
   int64_t guard;      // guard chunks before and after the cells (>= one plane + one row + 1)
+  int swap;           // 0: rows run along x (s0 = x, s1 = y); 1: rows run along y (s0 = y,
+                      // s1 = x; lbm_desc.row_axis) -- c = s0 - xshift + s1*pitch + zs*plane,
+                      // pitch >= the row length, plane = pitch * the row count
   // population buffers: guard + nchunk + guard chunks; the base pointer skips the leading
   // guard, so the pulls of lanes masked out at the range ends never leave the allocation
   int64_t buf_floats() const { return (nchunk + 2 * guard) * kQ * kChunk; }
@@ -79,6 +82,7 @@ struct MainArgs {
   int nee_blocks;       // multiple of 8 (keeps the chunk blocks' XCD order)
   int nee_active;       // 0 at step 0: NEE cells are pulled raw (boundary_stream has not run)
   float omc;            // the reference's (1.0f - 1.0f / tau)
+  int swap;             // 1: storage rows run along physical y (Layout::swap)
 };
 
 // True when k_step's fast quotient (q0 = x*y, q = fma(fma(-q0, tau, x), y, q0),
@@ -125,7 +129,7 @@ hipError_t launch_unpack(float* f, const float* buf, const uint8_t* type, int zs
                          int nq, unsigned skip_classes, hipStream_t s);
 // seed wall slots with bounce-back values of buffer f (LDC: bounce-back already at step 0)
 hipError_t launch_bb_prime(float* f, const uint8_t* type, const uint32_t* links, int64_t ncell, int pitch,
-                           int64_t plane, hipStream_t s);
+                           int64_t plane, int swap, hipStream_t s);
 
 // LBM_CASE_GENERIC boundary code on the device (lbm_bc_code with a device table)
 struct BcCode {
@@ -148,27 +152,30 @@ struct GeoArgs {
   int nx, ny, pitch, xshift, planes;
   int64_t plane, ncell;
   int z_offset, nz_global;
+  int swap;                // Layout::swap
   BcCode bcs[kMaxBcCodes];  // LBM_CASE_GENERIC
   int nbc;
 };
 hipError_t launch_classify(const GeoArgs& g, hipStream_t s);
 hipError_t launch_flag_fluid(const GeoArgs& g, hipStream_t s);
 hipError_t launch_ldc_codes(int8_t* codes, int nx, int ny, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
-                            int nz_global, hipStream_t s);
+                            int nz_global, int swap, hipStream_t s);
 
 // initial populations from per-cell fields (nullable -> rho 1, u 0); form 0 = LDC wi form,
 // 1 = expanded; writes both buffers for every cell
 // geo_pre of a raw 0/1 mask on the device (bifurcation.cu:63-239): mask planes are global
 // z = zbase .. ; local storage planes z_lo .. z_hi-1 get codes (-1 for the halo plane below)
 hipError_t launch_mask_hist(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int z_lo, int z_hi,
-                            unsigned long long* hist, hipStream_t s);
+                            unsigned long long* hist, int swap, hipStream_t s);
 hipError_t launch_mask_codes(const uint8_t* mask, int nx, int ny, int nz_global, int zbase, int8_t* codes, int pitch,
-                             int xshift, int64_t plane, int64_t ncell, int z_offset, int z_lo, int z_hi, hipStream_t s);
+                             int xshift, int64_t plane, int64_t ncell, int z_offset, int z_lo, int z_hi, int swap,
+                             hipStream_t s);
 hipError_t launch_init_feq(float* fa, float* fb, int64_t ncell, int form, const float* rho, const float* ux,
                            const float* uy, const float* uz, hipStream_t s);
 hipError_t launch_init_mask(float* fa, float* fb, const int8_t* codes, const float* in_uy, const float* out_uy, int nx,
-                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset,
+                            int ny, int nz, int pitch, int xshift, int64_t plane, int64_t ncell, int z_offset, int swap,
                             hipStream_t s);
-hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int ny, float lid_u, hipStream_t s);
+hipError_t launch_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshift, int nx, int ny, float lid_u, int swap,
+                           hipStream_t s);
 
 }  // namespace lbm

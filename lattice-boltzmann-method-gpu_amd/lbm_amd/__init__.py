@@ -73,6 +73,7 @@ class lbm_desc(C.Structure):
         ("bc_codes", C.POINTER(lbm_bc_code)),
         ("n_bc_codes", C.c_int),
         ("mask", C.POINTER(C.c_uint8)),
+        ("row_axis", C.c_int),
     ]
 
 
@@ -81,6 +82,7 @@ LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_init_case", "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
+    "lbm_get_layout",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
 ]
 HOST_SYMBOLS = [
@@ -160,6 +162,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_kernel_times": (C.c_int, [P, C.c_int, f64p, i64p]),
             "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
             "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
+            "lbm_get_layout": (C.c_int, [P, ip, ip, ip, i64p]),
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
@@ -285,7 +288,7 @@ class Lattice:
     def __init__(self, case_kind: int, shape, tau: float, geo: np.ndarray | None = None, *,
                  halo_planes: bool = False, lid_u_val: float | None = None, inlet_uy=None, outlet_uy=None,
                  device: int = 0, z_offset: int = 0, nz_global: int | None = None, x_align: int = 0,
-                 bc_codes=None, mask: np.ndarray | None = None):
+                 bc_codes=None, mask: np.ndarray | None = None, row_axis: int = 0):
         """mask (LBM_CASE_MASK, geo None): raw geo.txt mask, uint8 [nz (+6 with halo_planes)][ny][nx];
         geo_pre runs on the device (lbm_desc.mask)."""
         nz, ny, nx = shape
@@ -321,6 +324,7 @@ class Lattice:
         d.z_offset = z_offset
         d.nz_global = nz if nz_global is None else nz_global
         d.x_align = x_align
+        d.row_axis = row_axis
         if bc_codes:
             arr = (lbm_bc_code * len(bc_codes))()
             for k, b in enumerate(bc_codes):
@@ -419,6 +423,14 @@ class Lattice:
         ns = C.c_int64()
         self._ck(lbm_lib().lbm_get_boundary_cells(self.h, C.byref(ns)), "lbm_get_boundary_cells")
         return {"n_box": nb.value, "n_fluid": nf.value, "algo_bytes_per_step": by.value, "n_boundary": ns.value}
+
+    def layout(self):
+        """Device layout lbm_create chose: row axis (1 x, 2 y), row pitch, x_align (1..4),
+        256-cell chunks holding fluid."""
+        ra, pitch, xa, nch = C.c_int(), C.c_int(), C.c_int(), C.c_int64()
+        self._ck(lbm_lib().lbm_get_layout(self.h, C.byref(ra), C.byref(pitch), C.byref(xa), C.byref(nch)),
+                 "lbm_get_layout")
+        return {"row_axis": ra.value, "pitch": pitch.value, "x_align": xa.value, "active_chunks": nch.value}
 
     def numerics(self):
         """(fast_div in use, chunks re-done on the exact division path since creation)."""

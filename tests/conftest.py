@@ -44,3 +44,11 @@ def cells_per_lane(request, monkeypatch):
     bandwidth path) and one cell per lane (what small lattices use by default)."""
     monkeypatch.setenv("LBM_CELLS_PER_LANE", request.param)
     return int(request.param)
+
+
+@pytest.fixture(params=["x", "y"], ids=["xrows", "yrows"])
+def row_axis(request, monkeypatch):
+    """Run a parity test on both device layouts: rows along x and rows along y
+    (lbm_desc.row_axis; LBM_ROW_AXIS stands in for row_axis = 0)."""
+    monkeypatch.setenv("LBM_ROW_AXIS", request.param)
+    return request.param

@@ -48,7 +48,7 @@ def test_device_geo_bifurcation(gpu, oracle):
 
 
 @pytest.mark.parametrize("shape", [(23, 31, 37), (12, 9, 13), (30, 40, 66)])
-def test_device_geo_vessels_and_noise(gpu, oracle, shape):
+def test_device_geo_vessels_and_noise(gpu, oracle, shape, row_axis):
     from lbm_amd import cases
     for raw in (vessel_mask(shape, 1), (np.random.default_rng(2).random(shape) < 0.75).astype(np.uint8)):
         lat = cases.mask_device(raw)
@@ -59,7 +59,7 @@ def test_device_geo_vessels_and_noise(gpu, oracle, shape):
 
 
 @pytest.mark.parametrize("shape", [(23, 31, 37), (30, 40, 66)])
-def test_device_mask_lattice_bitwise(gpu, oracle, shape, cells_per_lane):
+def test_device_mask_lattice_bitwise(gpu, oracle, shape, cells_per_lane, row_axis):
     """Device codes + device initialize() vs the oracle (and the host path) over 60 steps."""
     from lbm_amd import cases, geo_mask, initial_fields, Lattice, LBM_CASE_MASK, LBM_INIT_EXPANDED
     raw = vessel_mask(shape, 3)
@@ -93,7 +93,7 @@ def test_device_bifurcation_matches_host(gpu):
 
 
 @pytest.mark.parametrize("nslabs", [2, 3])
-def test_device_mask_slabs(gpu, nslabs):
+def test_device_mask_slabs(gpu, nslabs, row_axis):
     """Halo slabs built from slab_mask (3 extra planes each side): each slab's codes are the
     global codes of its planes, and the loopback slab run equals the single domain."""
     from lbm_amd import cases, geo_mask, x_align_for, LBM_CASE_MASK

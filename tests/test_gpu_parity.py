@@ -44,7 +44,7 @@ def assert_residuals(hg, ho):
 
 
 @pytest.mark.parametrize("n,steps", [(16, [1, 1, 5, 40]), (32, [1, 3, 100]), (64, [2, 150])])
-def test_ldc_bitwise(gpu, oracle, n, steps, cells_per_lane):
+def test_ldc_bitwise(gpu, oracle, n, steps, cells_per_lane, row_axis):
     from lbm_amd import cases
     lat, geo = cases.ldc(n)
     o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
@@ -55,12 +55,14 @@ def test_ldc_bitwise(gpu, oracle, n, steps, cells_per_lane):
         assert_residuals(hg, ho)
 
 
-def test_fast_division_domain_retry(gpu, oracle, monkeypatch):
+@pytest.mark.parametrize("axis", ["x", "y"])
+def test_fast_division_domain_retry(gpu, oracle, monkeypatch, axis):
     """Populations outside the fast quotient's proven domain (a tiny f, a huge f) make their
     waves re-run on the exact-division path in the same step: still bit-identical, and the
     re-done chunks are counted.  Cells chosen next to the lid (NEE fix-up) and a wall."""
     from lbm_amd import cases
     monkeypatch.setenv("LBM_CELLS_PER_LANE", "4")  # the fast division lives on the 4-cell path
+    monkeypatch.setenv("LBM_ROW_AXIS", axis)
     n = 32
     lat, geo = cases.ldc(n)
     assert lat.numerics()["fast_div"]
@@ -104,7 +106,7 @@ def test_initial_state_bitwise(gpu, oracle):
 
 @pytest.mark.parametrize("shape,steps", [((32, 32, 32), [1, 2, 60]), ((24, 40, 24), [1, 90]),
                                          ((64, 64, 64), [1, 120])])
-def test_poiseuille_bitwise(gpu, oracle, shape, steps, cells_per_lane):
+def test_poiseuille_bitwise(gpu, oracle, shape, steps, cells_per_lane, row_axis):
     from lbm_amd import cases
     nx, ny, nz = shape
     lat, geo = cases.poiseuille(nx, ny, nz)
@@ -117,7 +119,7 @@ def test_poiseuille_bitwise(gpu, oracle, shape, steps, cells_per_lane):
 
 
 @pytest.mark.parametrize("block", [0, 1])
-def test_bifurcation_bitwise(gpu, oracle, block, cells_per_lane):
+def test_bifurcation_bitwise(gpu, oracle, block, cells_per_lane, row_axis):
     from lbm_amd import cases
     lat, geo, inl, outl = cases.bifurcation(block)
     o = oracle.Oracle(oracle.MASK, geo, 0.55, inlet_uy=inl, outlet_uy=outl)
@@ -189,7 +191,7 @@ def test_convergence_loop(gpu, oracle):
 
 
 @pytest.mark.parametrize("nslabs", [2, 3])
-def test_loopback_slabs_bitwise(gpu, nslabs, cells_per_lane):
+def test_loopback_slabs_bitwise(gpu, nslabs, cells_per_lane, row_axis):
     """z-slab decomposition with halo exchange (5 populations per face) == one domain."""
     from lbm_amd import cases, initial_fields, Lattice, LBM_CASE_POISEUILLE, LBM_INIT_EXPANDED
     import lbm_amd
@@ -299,7 +301,7 @@ def test_fast_division_retry_large(gpu, oracle):
 
 
 @pytest.mark.parametrize("shape", [(24, 14, 12), (40, 22, 18)])
-def test_generic_boundaries_bitwise(gpu, oracle, shape, cells_per_lane):
+def test_generic_boundaries_bitwise(gpu, oracle, shape, cells_per_lane, row_axis):
     """LBM_CASE_GENERIC: inlet (+x, velocity + rho, per-cell table), outlet (-x, velocity),
     side outlet (-z) and a pressure patch (+y) -- coronary.cu:716-944's scheme on every kind
     of face -- bit for bit against the oracle's generic restatement."""
@@ -339,7 +341,7 @@ def test_coronary_codes_bitwise(gpu, oracle):
 
 
 @pytest.mark.parametrize("shape", [(37, 29, 23), (13, 11, 7), (66, 9, 31)])
-def test_ragged_shapes_bitwise(gpu, oracle, shape, cells_per_lane):
+def test_ragged_shapes_bitwise(gpu, oracle, shape, cells_per_lane, row_axis):
     """Extents that are not multiples of 4 (row padding, row shift, chunks straddling rows
     and planes) and very flat boxes."""
     from lbm_amd import cases
@@ -356,7 +358,7 @@ def test_ragged_shapes_bitwise(gpu, oracle, shape, cells_per_lane):
     assert_bitwise(lat, o, geo, 1, f"poiseuille {shape}")
 
 
-def test_thin_slabs_loopback(gpu):
+def test_thin_slabs_loopback(gpu, row_axis):
     """Slabs of one and two planes (edge ranges overlapping / covering the whole slab)."""
     from lbm_amd import cases
     import lbm_amd
@@ -373,7 +375,7 @@ def test_thin_slabs_loopback(gpu):
             assert np.array_equal(a.view(np.uint32), b[z0:z1].view(np.uint32))
 
 
-def test_rccl_single_rank_step_path(gpu, cells_per_lane):
+def test_rccl_single_rank_step_path(gpu, cells_per_lane, row_axis):
     """lbm_attach_rccl with one rank: the multi-GPU step (edge planes then interior on two
     streams, halo pack/unpack, residual all-reduce + device finisher) with no peers -- must
     match the single-domain step bit for bit, residuals included."""
@@ -394,3 +396,26 @@ def test_rccl_single_rank_step_path(gpu, cells_per_lane):
     b.step(100)
     assert a.state()["k"] == b.state()["k"] == 61
     b.close()
+
+
+def test_row_axis_choice(gpu, oracle):
+    """lbm_desc.row_axis = 0 picks rows along y for a pipe along y (whole fluid rows: fewer
+    active chunks) and x for the cavity; an explicit row_axis in the descriptor is honoured
+    and bit-identical to the oracle."""
+    from lbm_amd import cases, Lattice, LBM_CASE_LDC, LBM_INIT_LDC_WI, initial_fields
+    lat, geo = cases.poiseuille(32, 256, 32)
+    lay = lat.layout()
+    assert lay["row_axis"] == 2 and lay["pitch"] == 256, lay
+    geo_x = Lattice(lat.case_kind, geo.shape, 0.58, geo, row_axis=1).layout()
+    assert lay["active_chunks"] < 0.8 * geo_x["active_chunks"], (lay, geo_x)
+    lat, _ = cases.ldc(24)
+    assert lat.layout()["row_axis"] == 1
+    assert cases.ldc_device(24, 24, 24).layout()["row_axis"] == 1
+    geo = __import__("lbm_amd").geo_ldc(22, 30, 26)
+    lat = Lattice(LBM_CASE_LDC, geo.shape, 0.55, geo, row_axis=2)
+    assert lat.layout()["row_axis"] == 2 and lat.layout()["pitch"] == 32
+    lat.init_equilibrium(LBM_INIT_LDC_WI, *initial_fields(0, geo))
+    o = oracle.Oracle(oracle.LDC, geo, 0.55)
+    lat.step(21, history=False)
+    o.step(21)
+    assert_bitwise(lat, o, geo, 0, "ldc row_axis 2")
