@@ -414,7 +414,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
-  L.swap = choose_swap(c->d);
+  L.swap = choose_swap(d);  // the caller's desc: c->d no longer holds geo / mask
   L.xshift = choose_xshift(d, L.swap);
   L.pitch = ((L.swap ? d.ny : d.nx) + 3) / 4 * 4;
   L.planes = d.nz + 2;
