@@ -36,10 +36,12 @@ constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom 
 struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) with their work lists
   int64_t c_lo = 0, c_hi = 0, c_lo2 = 0, c_hi2 = 0;
   int* chunks = nullptr;  // active 256-cell chunks (>= 1 fluid cell in range)
+  int chunk0 = -1;        // >= 0: chunks is chunk0, chunk0 + 1, ... (the kernel skips the list)
   int nchunks = 0;
   int* cells = nullptr;   // NEE-adjacent fluid cells
   int nslow = 0;
   float4* prev = nullptr; // their (rho, u) of the previous step
+  uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
   int* retry = nullptr;   // fast-quotient domain misses: queued chunk ids (capacity nchunks)
@@ -247,17 +249,18 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, b
   a.type = c->type; a.links = c->links;
   a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
   a.partial = r.part;
-  a.chunks = r.chunks; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
+  a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.tau = c->tau;
   a.tau_rcp = 1.0f / c->tau;
   a.fast_div = (c->fast_div && allow_fast && r.retry && !r.quarter) ? 1 : 0;
+  a.tau_fast = c->fast_div ? 1 : 0;
   a.retry = r.retry;
   a.retry_count = a.fast_div ? r.retry_cnt : nullptr;
   a.store_all_macros = store_all ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
-  a.cells = r.cells; a.prev = r.prev; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
+  a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
   a.nee_active = hstep == 0 ? 0 : 1;
   a.omc = c->omc;
   a.swap = c->L.swap;
@@ -293,6 +296,9 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   scan(lo, hi);
   if (hi2 > lo2) scan(lo2, hi2);
   r.nchunks = (int)chunks.size();
+  r.chunk0 = chunks.empty() ? -1 : chunks[0];
+  for (size_t i = 1; i < chunks.size() && r.chunk0 >= 0; ++i)
+    if (chunks[i] != chunks[0] + (int)i) r.chunk0 = -1;
   r.nslow = (int)cells.size();
   if (r.nchunks) {
     HIPCK(c, hipMalloc(&r.chunks, sizeof(int) * r.nchunks));
@@ -303,6 +309,47 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMemcpy(r.cells, cells.data(), sizeof(int) * r.nslow, hipMemcpyHostToDevice));
     HIPCK(c, hipMalloc(&r.prev, sizeof(float4) * r.nslow));
     HIPCK(c, hipMemset(r.prev, 0, sizeof(float4) * r.nslow));
+    // which populations each cell takes from an NEE neighbour (the face test of
+    // boundary_stream: q crosses the boundary cell's face, e_q . n == 1), resolved once here
+    // so that the kernel issues every load of such a cell in one round trip
+    std::vector<uint2> nm(cells.size());
+    int64_t off[kQ];
+    for (int q = 0; q < kQ; ++q) {
+      const int s0 = c->L.swap ? kEy[q] : kEx[q], s1 = c->L.swap ? kEx[q] : kEy[q];
+      off[q] = s0 + (int64_t)s1 * c->L.pitch + (int64_t)kEz[q] * c->L.plane;
+    }
+    for (size_t i = 0; i < cells.size(); ++i) {
+      uint32_t nee = 0, press = 0;
+      for (int q = 1; q < kQ; ++q) {
+        const int64_t nb = cells[i] - off[q];
+        if (nb < 0 || nb >= (int64_t)t.size()) continue;
+        const uint8_t tn = t[nb];
+        if ((tn & kClassMask) != kNee) continue;
+        const int fb = (kEx[q] == 1 ? 1 : 0) | (kEx[q] == -1 ? 2 : 0) | (kEy[q] == 1 ? 4 : 0) |
+                       (kEy[q] == -1 ? 8 : 0) | (kEz[q] == 1 ? 16 : 0) | (kEz[q] == -1 ? 32 : 0);
+        if (!((fb >> nee_face(tn)) & 1)) continue;
+        nee |= 1u << q;
+        if (tn & kKindPressure) press |= 1u << q;
+      }
+      nm[i] = make_uint2(nee, press);
+    }
+    // group cells with the same directions (inlet / outlet / lid faces, edges) so that the
+    // lanes of a wave take the same branches; cell order within a group
+    std::vector<size_t> perm(cells.size());
+    for (size_t i = 0; i < perm.size(); ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](size_t x, size_t y) {
+      return nm[x].x != nm[y].x ? nm[x].x < nm[y].x : nm[x].y < nm[y].y;
+    });
+    std::vector<int> sc(cells.size());
+    std::vector<uint2> snm(cells.size());
+    for (size_t i = 0; i < perm.size(); ++i) {
+      sc[i] = cells[perm[i]];
+      snm[i] = nm[perm[i]];
+    }
+    HIPCK(c, hipMemcpy(r.cells, sc.data(), sizeof(int) * r.nslow, hipMemcpyHostToDevice));
+    nm.swap(snm);
+    HIPCK(c, hipMalloc(&r.nee_mask, sizeof(uint2) * r.nslow));
+    HIPCK(c, hipMemcpy(r.nee_mask, nm.data(), sizeof(uint2) * r.nslow, hipMemcpyHostToDevice));
   }
   {
     const char* e = std::getenv("LBM_CELLS_PER_LANE");  // A/B switch: 1 or 4 (default: by size)
@@ -323,6 +370,7 @@ void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
+  if (r.nee_mask) (void)hipFree(r.nee_mask);
   if (r.retry) (void)hipFree(r.retry);
   if (r.retry_cnt) (void)hipFree(r.retry_cnt);
   r = Range{};

@@ -158,6 +158,42 @@ template <> LBM_HD float feq_bc<14>(float tmp_rho, float tmp_ux, float tmp_uy, f
   return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz -1.5f* tmp_uy*tmp_uy);
 }
 
+// f^eq_q for a run-time q (1..18), branch-free, bit-identical to feq<q> (bc_form = false)
+// or feq_bc<q> (bc_form = true).  The reference's 18 expression trees share two shapes:
+//   axis q (e along axis a, sign s):  r/18 * (1 + 3A + 3A*A - 1.5 ub*ub - 1.5 uc*uc)
+//   diagonal q (axes a < b, signs):   r/36 * (1 + 3(A+B) + 3A*A + 3B*B + 9A*B - 1.5 uc*uc)
+// with A = s_a u_a, B = s_b u_b and (b, c) / c the remaining axes in x, y, z order.  Signs
+// enter exactly: x - y == x + (-y), -(x + y) == (-x) + (-y), (kx)(-y) == -((kx)y) and
+// addition commutes in IEEE arithmetic, so e.g. "1 - 3(ux+uy)" (q = 10) and
+// "3(uy - ux)" (q = 9) come out bit for bit.  The update form of q = 14 (the one with an
+// fp64 sub-expression) is taken from feq<14> itself.  Checked against every feq<q> /
+// feq_bc<q> on random and special inputs by tests/test_host_ingest.py (tools/feq_rt_check.cpp).
+constexpr uint64_t pack_e(const int* e) {
+  uint64_t p = 0;
+  for (int q = 0; q < 19; ++q) p |= (uint64_t)(e[q] + 1) << (2 * q);
+  return p;
+}
+constexpr uint64_t kPackEx = pack_e(kEx), kPackEy = pack_e(kEy), kPackEz = pack_e(kEz);
+LBM_HD int e_of(uint64_t packed, int q) { return (int)((packed >> (2 * q)) & 3u) - 1; }
+
+LBM_HD float feq_rt(int q, float r, float ux, float uy, float uz, bool bc_form) {
+  if (!bc_form && q == 14) return feq<14>(r, ux, uy, uz);
+  const int ex = e_of(kPackEx, q), ey = e_of(kPackEy, q), ez = e_of(kPackEz, q);
+  if (ex * ex + ey * ey + ez * ez == 1) {
+    const float ua = ex ? ux : ey ? uy : uz;
+    const float A = (ex + ey + ez) < 0 ? -ua : ua;
+    const float ub = ex ? uy : ux;   // a = x: (y, z); a = y: (x, z); a = z: (x, y)
+    const float uc = ez ? uy : uz;
+    return r / 18.0f * (1.0f + 3.0f * A + 3.0f * A * A - 1.5f * ub * ub - 1.5f * uc * uc);
+  }
+  const float ua = ex ? ux : uy;     // first non-zero axis
+  const float ub = ez ? uz : uy;     // second non-zero axis
+  const float uc = !ex ? ux : !ey ? uy : uz;
+  const int sa = ex ? ex : ey, sb = ez ? ez : ey;
+  const float A = sa < 0 ? -ua : ua, B = sb < 0 ? -ub : ub;
+  return r / 36.0f * (1.0f + 3.0f * (A + B) + 3.0f * A * A + 3.0f * B * B + 9.0f * A * B - 1.5f * uc * uc);
+}
+
 // The LDC initialize() form (ldc.cu:542-571): all 19 at once.
 LBM_HD void feq_init_wi(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz, float* feq) {
   const float w0 = 1.0f / 3.0f, w1 = 1.0f / 18.0f, w2 = 1.0f / 36.0f;

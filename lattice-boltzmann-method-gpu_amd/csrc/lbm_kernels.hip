@@ -317,42 +317,139 @@ struct Macro {
   float rho, ux, uy, uz;
 };
 
+// NEE-supplied pulls (boundary cell B = c - e_q with e_q . n_B == 1), in two phases so
+// that all of a cell's loads are in flight together: which q come from an NEE neighbour is
+// static (nee_mask, built with the work lists), so no load waits on another.
+//   issue: the 19 pulls, and for the first kNeeSlots NEE directions the cell's own src
+//          slot and B's boundary data (u_bc, and rho_bc or NaN; a pressure cell's rho_bc);
+//   apply: f_q = feq_q(rho_bc, u_bc) + (own - feq_q(rho_c, u_c)) (1 - 1/tau), with the
+//          cell's own (rho, u) of the previous step.
+// A cell beside one flat face has 5 NEE directions; cells with more (edges, corners of
+// several boundary faces) load the rest where they are used.
+constexpr int kNeeSlots = 5;
+
+template <bool SW>
+__device__ __forceinline__ int64_t cell_off_rt(int q, int pitch, int64_t plane) {
+  const int ex = e_of(kPackEx, q), ey = e_of(kPackEy, q), ez = e_of(kPackEz, q);
+  return (SW ? ey : ex) + (int64_t)(SW ? ex : ey) * pitch + (int64_t)ez * plane;
+}
+
+struct NeeSlot {
+  float own, r, x, y, z;
+};
+
+template <bool SW>
+__device__ __forceinline__ NeeSlot nee_load(const MainArgs& a, int64_t c, int64_t nb, int q) {
+  return NeeSlot{a.src[aidx(c, q)], a.rho[nb], a.ux[nb], a.uy[nb], a.uz[nb]};
+}
+
+// the NEE value of direction Q from its slot
+template <int Q>
+__device__ __forceinline__ float nee_value(const NeeSlot& d, const Macro& mp, bool pressure, float omc) {
+  float rb = d.r, bx, by, bz;
+  if (pressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
+    bx = mp.ux; by = mp.uy; bz = mp.uz;
+  } else {         // u_bc stored at B; rho_bc too, or NaN: that of the fluid cell
+    if (__builtin_isnan(rb)) rb = mp.rho;
+    bx = d.x; by = d.y; bz = d.z;
+  }
+  const float e_bc = feq_bc<Q>(rb, bx, by, bz);
+  const float e_nb = feq<Q>(mp.rho, mp.ux, mp.uy, mp.uz);
+  return e_bc + (d.own - e_nb) * omc;
+}
+
+// run-time q (the slot's direction): the branch-free feq_rt, so lanes with different
+// directions stay together
+__device__ __forceinline__ float nee_value_rt(int q, const NeeSlot& d, const Macro& mp, bool pressure, float omc) {
+  float rb = d.r, bx, by, bz;
+  if (pressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
+    bx = mp.ux; by = mp.uy; bz = mp.uz;
+  } else {         // u_bc stored at B; rho_bc too, or NaN: that of the fluid cell
+    if (__builtin_isnan(rb)) rb = mp.rho;
+    bx = d.x; by = d.y; bz = d.z;
+  }
+  const float e_bc = feq_rt(q, rb, bx, by, bz, true);
+  const float e_nb = feq_rt(q, mp.rho, mp.ux, mp.uy, mp.uz, false);
+  return e_bc + (d.own - e_nb) * omc;
+}
+
+// f[Q] from the k-th NEE value (k = rank of Q among the cell's NEE directions)
 template <int Q, bool SW>
-__device__ __forceinline__ void fix_pull(float* f, const MainArgs& a, int64_t c, const Macro& mp) {
-  const int64_t nb = c - cell_off<Q, SW>(a.pitch, a.plane);
-  f[Q] = a.src[aidx(nb, Q)];
-  if constexpr (Q == 0) return;
-  const uint8_t tn = a.type[nb];
-  const int cls = tn & kClassMask;
-  if (cls == kNee) {
-    if (a.nee_active && ((face_bits<Q>() >> nee_face(tn)) & 1)) {
-      float rb, bx, by, bz;
-      if (tn & kKindPressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
-        rb = a.rho[nb];
-        bx = mp.ux; by = mp.uy; bz = mp.uz;
-      } else {                   // u_bc stored at B; rho_bc stored too, or NaN: that of the fluid cell
-        rb = a.rho[nb];
-        if (__builtin_isnan(rb)) rb = mp.rho;
-        bx = a.ux[nb]; by = a.uy[nb]; bz = a.uz[nb];
-      }
-      const float own = a.src[aidx(c, Q)];
-      const float e_bc = feq_bc<Q>(rb, bx, by, bz);
-      const float e_nb = feq<Q>(mp.rho, mp.ux, mp.uy, mp.uz);
-      f[Q] = e_bc + (own - e_nb) * a.omc;
+__device__ __forceinline__ void nee_put(float* f, const float* nv, const MainArgs& a, int64_t c, const Macro& mp,
+                                        uint32_t nee, uint32_t press) {
+  if constexpr (Q > 0) {
+    if (nee & (1u << Q)) {
+      const int k = __builtin_popcount(nee & ((1u << Q) - 1u));
+      float v = nv[0];
+#pragma unroll
+      for (int j = 1; j < kNeeSlots; ++j)
+        if (k == j) v = nv[j];
+      if (k >= kNeeSlots)  // beyond the slots (edges/corners of several faces): load here
+        v = nee_value<Q>(nee_load<SW>(a, c, c - cell_off<Q, SW>(a.pitch, a.plane), Q), mp, (press >> Q) & 1u,
+                         a.omc);
+      f[Q] = v;
     }
   }
 }
 
 template <bool SW, int... Qs>
-__device__ __forceinline__ void fix_pull_all(float* f, const MainArgs& a, int64_t c, const Macro& mp,
+__device__ __forceinline__ void nee_pull_all(float* f, const MainArgs& a, int64_t c, const Macro& mp, uint2 m,
                                              std::integer_sequence<int, Qs...>) {
-  (fix_pull<Qs, SW>(f, a, c, mp), ...);
+  const uint32_t nee = a.nee_active ? m.x : 0u;
+  NeeSlot sl[kNeeSlots];
+  int qs[kNeeSlots];
+  uint32_t rest = nee;
+#pragma unroll
+  for (int j = 0; j < kNeeSlots; ++j) {
+    qs[j] = 0;
+    if (rest) {
+      const int q = __builtin_ctz(rest);
+      rest &= rest - 1u;
+      qs[j] = q;
+      sl[j] = nee_load<SW>(a, c, c - cell_off_rt<SW>(q, a.pitch, a.plane), q);
+    }
+  }
+  ((f[Qs] = a.src[aidx(c - cell_off<Qs, SW>(a.pitch, a.plane), Qs)]), ...);
+  if (!nee) return;
+  float nv[kNeeSlots];
+#pragma unroll
+  for (int j = 0; j < kNeeSlots; ++j)
+    nv[j] = qs[j] ? nee_value_rt(qs[j], sl[j], mp, (m.y >> qs[j]) & 1u, a.omc) : 0.f;
+  (nee_put<Qs, SW>(f, nv, a, c, mp, nee, m.y), ...);
 }
 
 template <int... Qs>
 __device__ __forceinline__ void fix_relax_all(float* f, float tau, float r, float ux, float uy, float uz,
                                               std::integer_sequence<int, Qs...>) {
   ((f[Qs] = f[Qs] - (f[Qs] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
+}
+// the same with relax_cell's 3-VALU quotient (caller: tau verified, cell in the domain)
+template <int... Qs>
+__device__ __forceinline__ void fix_relax_fast_all(float* f, float tau, float rcp, float r, float ux, float uy,
+                                                   float uz, std::integer_sequence<int, Qs...>) {
+  auto div_tau = [&](float x) {
+    const float q0 = x * rcp;
+    return __builtin_fmaf(__builtin_fmaf(-q0, tau, x), rcp, q0);
+  };
+  ((f[Qs] = f[Qs] - div_tau(f[Qs] - feq<Qs>(r, ux, uy, uz))), ...);
+}
+// fast_div_ok for one cell in registers
+__device__ __forceinline__ bool fast_div_ok1(const float* f, float ux, float uy, float uz) {
+  float mn = __builtin_fabsf(f[0]), mx = mn;
+#pragma unroll
+  for (int q = 1; q < kQ; ++q) {
+    mn = __builtin_fminf(mn, __builtin_fabsf(f[q]));
+    mx = __builtin_fmaxf(mx, __builtin_fabsf(f[q]));
+  }
+  const float um = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ux), __builtin_fabsf(uy)), __builtin_fabsf(uz));
+  return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f;  // false for NaN
+}
+// one cell's relaxation: the fast quotient when tau is verified and every active lane of
+// the wave lies in its domain (a wave-uniform choice: the lanes stay together), else exact
+__device__ __forceinline__ void relax1(float* f, const MainArgs& a, float r, float ux, float uy, float uz) {
+  const bool ok = fast_div_ok1(f, ux, uy, uz);
+  if (a.tau_fast && __all(ok)) fix_relax_fast_all(f, a.tau, a.tau_rcp, r, ux, uy, uz, AllQ{});
+  else fix_relax_all(f, a.tau, r, ux, uy, uz, AllQ{});
 }
 template <bool SW, int... Qs>
 __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m,
@@ -370,16 +467,17 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const int64_t c = a.cells[i];
   const float4 pv = a.prev[i];
   const Macro mp{pv.x, pv.y, pv.z, pv.w};
+  const uint32_t links = a.links[c];
   float f[kQ];
-  fix_pull_all<SW>(f, a, c, mp, AllQ{});
+  nee_pull_all<SW>(f, a, c, mp, a.nee_mask[i], AllQ{});
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
   const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
-  fix_store_all<SW>(f, a.dst, c, a.links[c], a.pitch, a.plane, AllQ{});
+  relax1(f, a, rho, ux, uy, uz);
+  fix_store_all<SW>(f, a.dst, c, links, a.pitch, a.plane, AllQ{});
   a.prev[i] = make_float4(rho, ux, uy, uz);
   if (a.store_all_macros) {
     a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
@@ -397,20 +495,23 @@ __device__ __forceinline__ void pull1_all(float* f, const float* __restrict__ sr
 
 template <bool SW>
 __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
+  // the pulls go out with the type byte (one round trip; the guard chunks keep every
+  // address of a lane that turns out to be idle inside the buffer)
   const uint8_t t = a.type[c];
+  const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
+  float f[kQ];
+  pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
   const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid &&
                   !(t & kNeedsMac);
   if (!in) return 0.0;
-  float f[kQ];
-  pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
   const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  fix_relax_all(f, a.tau, rho, ux, uy, uz, AllQ{});
-  fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? a.links[c] : 0u, a.pitch, a.plane, AllQ{});
+  relax1(f, a, rho, ux, uy, uz);
+  fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
   if (a.store_all_macros) {
     a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
   }
@@ -419,8 +520,24 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
 
 // ---- the step kernel -------------------------------------------------------------------
 
+__device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
+  // ldc.cu:662-684: residual = |S_k - S_{k-1}| / S_k on fp32 sums
+  const float sum_next = (float)S;
+  const float residual = fabsf(sum_next - cv->sum_current) / sum_next;
+  cv->residual = residual;
+  cv->sum_current = sum_next;
+  cv->k += 1;
+  if (residual <= cv->tol) cv->tol_count += 1;
+  if (cv->enabled) cv->stopped = !(cv->k <= cv->max_it && cv->tol_count <= cv->stag_max);
+  if (hist_slot) *hist_slot = residual;
+}
+
+__device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
+  return a.chunk0 >= 0 ? (int64_t)a.chunk0 + idx : (int64_t)a.chunks[idx];
+}
+
 template <bool FAST, bool QUARTER, bool SW>
-__global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
+__device__ __forceinline__ void step_body(const MainArgs& a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
   double acc = 0.0;
@@ -436,9 +553,9 @@ __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
     const int idx = slot * (kBlock / 64) + wave;
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
-        acc = process_cell1<SW>(a, (int64_t)a.chunks[idx >> 2] * kChunk + (idx & 3) * 64 + lane);
+        acc = process_cell1<SW>(a, chunk_of(a, idx >> 2) * kChunk + (idx & 3) * 64 + lane);
     } else if (idx < a.nchunks) {
-      acc = process_chunk<FAST, SW>(a, (int64_t)a.chunks[idx] * kChunk, lane);  // uniform base
+      acc = process_chunk<FAST, SW>(a, chunk_of(a, idx) * kChunk, lane);  // uniform base
     }
     slot += a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
@@ -450,19 +567,18 @@ __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
   if (threadIdx.x == 0) a.partial[slot] = s;
 }
 
-// ---- residual --------------------------------------------------------------------------
-
-__device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
-  // ldc.cu:662-684: residual = |S_k - S_{k-1}| / S_k on fp32 sums
-  const float sum_next = (float)S;
-  const float residual = fabsf(sum_next - cv->sum_current) / sum_next;
-  cv->residual = residual;
-  cv->sum_current = sum_next;
-  cv->k += 1;
-  if (residual <= cv->tol) cv->tol_count += 1;
-  if (cv->enabled) cv->stopped = !(cv->k <= cv->max_it && cv->tol_count <= cv->stag_max);
-  if (hist_slot) *hist_slot = residual;
+// 4 cells per lane (big lattices): two waves per SIMD, pinned by the LDS reservation
+template <bool FAST, bool SW>
+__global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
+  step_body<FAST, false, SW>(a);
 }
+// one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
+template <bool SW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_step1(const MainArgs a) {
+  step_body<false, true, SW>(a);
+}
+
+// ---- residual --------------------------------------------------------------------------
 
 // slice b of the block partials -> out[b]; then the chunks the fast path queued, re-done
 // with the exact division by all slice blocks together -> out[gridDim.x + b]
@@ -924,12 +1040,12 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   Kern k;
   size_t lds = kOccupancyLds;
   if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
-    k = sw ? k_step<false, true, true> : k_step<false, true, false>;
+    k = sw ? k_step1<true> : k_step1<false>;
     lds = 0;
   } else if (a.fast_div) {
-    k = sw ? k_step<true, false, true> : k_step<true, false, false>;
+    k = sw ? k_step<true, true> : k_step<true, false>;
   } else {
-    k = sw ? k_step<false, false, true> : k_step<false, false, false>;
+    k = sw ? k_step<false, true> : k_step<false, false>;
   }
   hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, a);
   return hipGetLastError();

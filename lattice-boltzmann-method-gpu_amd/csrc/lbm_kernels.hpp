@@ -60,6 +60,8 @@ struct MainArgs {
   float* rho; float* ux; float* uy; float* uz;  // full fields; NEE data sits at NEE cells
   double* partial;      // one per block
   const int* chunks;    // active chunk ids
+  int chunk0;           // >= 0: they are chunk0, chunk0 + 1, ... (box lattices) -- no list load,
+                        // one dependent round trip less per wave
   int nchunks;
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
   int quarter;          // 1: one cell per lane, a wave per 64-cell quarter chunk (small lattices)
@@ -70,7 +72,10 @@ struct MainArgs {
                         // outside them are not touched
   float tau;
   float tau_rcp;        // RN(1 / tau)
-  int fast_div;         // 1: tau passed verify_fast_div (3-VALU correctly rounded x / tau)
+  int fast_div;         // 1: the chunk path uses the 3-VALU quotient (tau passed
+                        // verify_fast_div), queueing waves outside its domain for a retry
+  int tau_fast;         // 1: tau passed verify_fast_div -- the one-cell paths (NEE cells,
+                        // one cell per lane) use the fast quotient wave by wave, else exact
   int* retry;           // fast_div: chunks whose wave left the fast quotient's domain ...
   int* retry_count;     // ... and their count (re-done exactly by the reduction launch)
   int store_all_macros;
@@ -78,6 +83,8 @@ struct MainArgs {
   // NEE-adjacent fluid cells
   const int* cells;     // linear ids
   float4* prev;         // per cell: its (rho, ux, uy, uz) of the previous step
+  const uint2* nee_mask;  // per cell: x bit q set when c - e_q is an NEE cell supplying q
+                          // (face match), y bit q when that cell is a pressure boundary
   int n_nee;
   int nee_blocks;       // multiple of 8 (keeps the chunk blocks' XCD order)
   int nee_active;       // 0 at step 0: NEE cells are pulled raw (boundary_stream has not run)
