@@ -197,6 +197,10 @@ def main():
         n_fluid_total = counts["n_fluid"]
     lat.close()
 
+    # attainable streaming bandwidth of this device, same run (context for roofline.frac:
+    # the 8 TB/s spec peak is not reached by any kernel)
+    probe = round(lbm_amd.probe_stream(local), 1) if rank == 0 else None
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -253,6 +257,11 @@ def main():
             "kernel_ms_per_step": round(main_step_ms, 4),
             "launches": main_n,
             "boundary_cells_per_gpu": counts["n_boundary"],
+            "stream_probe_gbs": probe,
+            "frac_of_stream_probe": round(achieved / probe, 4) if probe else None,
+            "stream_probe": "lbm_probe_stream: best of 7 streaming-copy shapes (16-B vectors, grid-stride or "
+                            "per-XCD regions, plain or non-temporal; read + write bytes / time) of 2 x 8 GiB "
+                            "on this GPU in this run",
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
         "residual_last": state["residual"],

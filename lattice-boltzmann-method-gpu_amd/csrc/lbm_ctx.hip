@@ -1023,6 +1023,47 @@ int lbm_stats(lbm_ctx* c, double* kernel_ms, int64_t* launches, double* algo_byt
   return LBM_OK;
 }
 
+int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
+  if (bytes < (1 << 16) || reps < 1 || !gbs) {
+    g_create_error = "lbm_probe_stream: bytes >= 64 KiB, reps >= 1, gbs non-null";
+    return LBM_ERR_ARG;
+  }
+  const int64_t n4 = (bytes >> 16) << 12;  // whole 64-KiB blocks of 16-B vectors
+  void *a = nullptr, *b = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  double best = 0.0;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&a, n4 * 16);
+  if (e == hipSuccess) e = hipMalloc(&b, n4 * 16);
+  if (e == hipSuccess) e = hipMemset(a, 0x3c, n4 * 16);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  const int shapes[][2] = {{8192, 0}, {8192, 1}, {8192, 2}, {8192, 3}, {4096, 4}, {2048, 5}, {32768, 2}};
+  for (const auto& sh : shapes) {  // blocks, launch_probe_copy shape
+    if (e != hipSuccess) break;
+    e = launch_probe_copy(a, b, n4, sh[0], sh[1], st);  // untimed first launch
+    for (int r = 0; r < reps && e == hipSuccess; ++r) {
+      e = hipEventRecord(e0, st);
+      if (e == hipSuccess) e = launch_probe_copy(r & 1 ? b : a, r & 1 ? a : b, n4, sh[0], sh[1], st);
+      if (e == hipSuccess) e = hipEventRecord(e1, st);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      float ms = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      if (e == hipSuccess && ms > 0.f) best = std::max(best, 2.0 * 16.0 * (double)n4 / (ms * 1e-3) / 1e9);
+    }
+  }
+  if (e != hipSuccess) g_create_error = std::string("lbm_probe_stream: ") + hipGetErrorString(e);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  *gbs = best;
+  return e == hipSuccess ? LBM_OK : LBM_ERR_HIP;
+}
+
 int lbm_rccl_unique_id(uint8_t out_id[128]) {
   if (!out_id) return LBM_ERR_ARG;
   ncclUniqueId id;

@@ -1069,6 +1069,48 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
   return hipGetLastError();
 }
 
+// XCD: workgroups are dealt round-robin to the 8 XCDs; block b takes the (b % 8)-th eighth
+// of the array, so each XCD streams one contiguous region (as k_step's chunk order does)
+template <int U, bool XCD, bool NT>
+__global__ __launch_bounds__(256) void k_probe_copy(const f4* __restrict__ a, f4* __restrict__ b, int64_t n4) {
+  int64_t lo = 0, hi = n4, first = blockIdx.x, nblk = gridDim.x;
+  if constexpr (XCD) {
+    const int64_t part = (n4 + 7) / 8;
+    lo = (blockIdx.x & 7) * part;
+    hi = lo + part < n4 ? lo + part : n4;
+    first = blockIdx.x >> 3;
+    nblk = gridDim.x >> 3;
+  }
+  const int64_t stride = nblk * blockDim.x;
+  for (int64_t i = lo + first * blockDim.x + threadIdx.x; i < hi; i += U * stride) {
+    f4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (i + k * stride < hi) v[k] = NT ? __builtin_nontemporal_load(a + i + k * stride) : a[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (i + k * stride < hi) {
+        if constexpr (NT) __builtin_nontemporal_store(v[k], b + i + k * stride);
+        else b[i + k * stride] = v[k];
+      }
+  }
+}
+
+hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks, int shape, hipStream_t s) {
+  const f4* a = static_cast<const f4*>(src);
+  f4* b = static_cast<f4*>(dst);
+  blocks = blocks / 8 * 8;
+  switch (shape) {
+    case 0: hipLaunchKernelGGL((k_probe_copy<1, false, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
+    case 1: hipLaunchKernelGGL((k_probe_copy<1, false, false>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
+    case 2: hipLaunchKernelGGL((k_probe_copy<1, true, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
+    case 3: hipLaunchKernelGGL((k_probe_copy<1, true, false>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
+    case 4: hipLaunchKernelGGL((k_probe_copy<2, true, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
+    default: hipLaunchKernelGGL((k_probe_copy<4, true, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s) {
   hipLaunchKernelGGL(k_finish_global, dim3(1), dim3(1), 0, s, conv, hist_slot);
   return hipGetLastError();

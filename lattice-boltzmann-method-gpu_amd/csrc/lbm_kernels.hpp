@@ -128,6 +128,12 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
                          double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
 
+// streaming copy of n4 16-B vectors (lbm_probe_stream): `blocks` x 256 threads; shape 0/1
+// grid-stride non-temporal / plain, 2/3 the same with one contiguous region per XCD, 4/5
+// XCD regions with 2 / 4 vectors in flight per thread
+constexpr int kProbeShapes = 6;
+hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks, int shape, hipStream_t s);
+
 // halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack
 hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const int* qs_dev, int nq,
                        hipStream_t s);

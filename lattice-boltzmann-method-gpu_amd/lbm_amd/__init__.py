@@ -83,7 +83,7 @@ LBM_SYMBOLS = [
     "lbm_init_case", "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
     "lbm_get_layout",
-    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step",
+    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step", "lbm_probe_stream",
 ]
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
@@ -166,6 +166,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
+            "lbm_probe_stream": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -454,6 +455,16 @@ class Lattice:
     def attach_rccl(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._ck(lbm_lib().lbm_attach_rccl(self.h, buf, rank, nranks), "lbm_attach_rccl")
+
+
+def probe_stream(device: int = 0, nbytes: int = 8 << 30, reps: int = 5) -> float:
+    """Best streaming-copy rate (read + write GB/s) of the device (lbm_probe_stream): the
+    attainable HBM bandwidth next to the 8 TB/s spec peak."""
+    gbs = C.c_double()
+    rc = lbm_lib().lbm_probe_stream(device, nbytes, reps, C.byref(gbs))
+    if rc != 0:
+        raise LbmError(f"lbm_probe_stream: {lbm_lib().lbm_last_error(None).decode()}")
+    return gbs.value
 
 
 def rccl_unique_id() -> bytes:
