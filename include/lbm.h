@@ -190,9 +190,9 @@ int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
  * fast_div = 1 when the 3-instruction correctly rounded quotient is in use (tau verified
  * exhaustively at lbm_create; LBM_EXACT_DIV=1 in the environment forces the compiler's
  * division).  A wave whose populations leave the quotient's proven domain (|f| outside
- * [2^-60, 2^40) or |u| >= 2^10, e.g. a diverging run) is re-done with the exact division in
- * the same step; retried_chunks counts those 256-cell chunks since creation.  Results are
- * bit-identical either way. */
+ * [2^-60, 2^40) or |u| >= 2^10, e.g. a diverging run) relaxes with the exact division
+ * instead (a wave-uniform branch in the same launch); retried_chunks counts those 256-cell
+ * chunk waves since creation.  Results are bit-identical either way. */
 int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
 /* The device layout lbm_create chose (lbm_desc.row_axis / x_align resolved): row_axis 1 = x,
  * 2 = y; pitch = row slots; x_align 1..4; active_chunks = 256-cell chunks k_step launches a

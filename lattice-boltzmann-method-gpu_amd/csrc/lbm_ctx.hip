@@ -44,8 +44,6 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
-  int* retry = nullptr;   // fast-quotient domain misses: queued chunk ids (capacity nchunks)
-  int* retry_cnt = nullptr;  // their count (emptied by the reduction launch)
   int main_blocks = 0, nee_blocks = 0;
   bool quarter = false;   // one cell per lane (small ranges)
 };
@@ -65,6 +63,9 @@ struct lbm_ctx {
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
   Range whole, edge, mid;  // single domain: whole; slabs: both edge planes (one launch), interior
   double* partial_all = nullptr;
+  double* red_part = nullptr;  // fused residual (one-cell single domain): 2 x red_n partials by step parity
+  int red_n = 0;               // whole.npart + 8 (the leading reduction group)
+  bool fuse_red = false;
   int npart_slab = 0;
   double* scratch = nullptr;
   ConvState* conv = nullptr;
@@ -79,7 +80,7 @@ struct lbm_ctx {
   int64_t n_box = 0, n_fluid = 0, n_slow = 0, n_wall_adj = 0;
   float tau = 0.f, omc = 0.f;
   bool fast_div = false;  // tau verified for the 3-VALU correctly rounded division
-  unsigned long long* retried = nullptr;  // device: chunks re-done on the exact path
+  unsigned long long* retried = nullptr;  // device: 4-cell waves that took the exact division
   // profiling
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -238,11 +239,14 @@ int harvest_profile(lbm_ctx* c) {
 }
 
 // one step's update of a range: ONE k_step launch (chunk blocks + NEE-adjacent cell blocks).
-// allow_fast = false keeps the exact division (slab edges: their halo is packed right after,
-// before the reduction that would re-do queued chunks).  *out: the arguments, for the
-// reduction's retry pass.
-int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, bool allow_fast = true,
-              MainArgs* out = nullptr) {
+// the previous step's residual folded into a launch (lbm_ctx::fuse_red)
+struct FusedRed {
+  double* part;        // this launch's partials
+  const double* prev;  // the previous launch's (nullptr: nothing to finish)
+  float* hist;         // the previous step's history slot (nullable)
+};
+
+int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, const FusedRed* fr = nullptr) {
   MainArgs a{};
   a.src = c->buf[hstep & 1];
   a.dst = c->buf[(hstep + 1) & 1];
@@ -254,24 +258,30 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, b
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.tau = c->tau;
   a.tau_rcp = 1.0f / c->tau;
-  a.fast_div = (c->fast_div && allow_fast && r.retry && !r.quarter) ? 1 : 0;
+  a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
   a.tau_fast = c->fast_div ? 1 : 0;
-  a.retry = r.retry;
-  a.retry_count = a.fast_div ? r.retry_cnt : nullptr;
+  a.exact_waves = c->retried;
   a.store_all_macros = store_all ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
   a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
   a.nee_active = hstep == 0 ? 0 : 1;
   a.omc = c->omc;
   a.swap = c->L.swap;
-  if (out) *out = a;
-  if (r.main_blocks + r.nee_blocks > 0) RCK(timed(c, st, 0, [&] { return launch_step(a, st); }));
+  if (fr) {
+    a.partial = fr->part;
+    a.red_blocks = 8;
+    a.red_partial = fr->prev;
+    a.red_n = c->red_n;
+    a.red_conv = c->conv;
+    a.red_hist = fr->hist;
+  }
+  if (r.main_blocks + r.nee_blocks > 0 || fr) RCK(timed(c, st, 0, [&] { return launch_step(a, st); }));
   return LBM_OK;
 }
 
 // work lists of the cells [lo, hi) u [lo2, hi2) from the host copy of the type bytes
 int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t, int64_t lo2 = 0,
-                int64_t hi2 = 0, bool with_retry = true) {
+                int64_t hi2 = 0) {
   if (lo2 < hi) lo2 = hi2 = 0;  // overlapping second interval (single-plane slab): drop it
   r.c_lo = lo;
   r.c_hi = hi;
@@ -357,11 +367,6 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   }
   r.main_blocks = main_grid(r.nchunks, r.quarter);
   r.nee_blocks = nee_grid(r.nslow);
-  if (c->fast_div && r.nchunks && with_retry) {
-    HIPCK(c, hipMalloc(&r.retry, sizeof(int) * r.nchunks));
-    HIPCK(c, hipMalloc(&r.retry_cnt, sizeof(int)));
-    HIPCK(c, hipMemset(r.retry_cnt, 0, sizeof(int)));
-  }
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }
@@ -371,8 +376,6 @@ void free_range(Range& r) {
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
   if (r.nee_mask) (void)hipFree(r.nee_mask);
-  if (r.retry) (void)hipFree(r.retry);
-  if (r.retry_cnt) (void)hipFree(r.retry_cnt);
   r = Range{};
 }
 
@@ -395,7 +398,6 @@ int reset_state(lbm_ctx* c) {
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
   for (Range* r : {&c->whole, &c->edge, &c->mid}) {
     if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
-    if (r->retry_cnt) HIPCK(c, hipMemset(r->retry_cnt, 0, sizeof(int)));
   }
   if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
     HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
@@ -632,12 +634,20 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     c->n_fluid = nf;
     const int64_t P = L.plane, nz = d.nz;
     if (build_range(c, c->whole, P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
-    if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P, false) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);
     if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t) != LBM_OK) return bail(LBM_ERR_HIP);
     // partial slots: [whole | lo | hi | mid]; the slab ranges are contiguous
     c->npart_slab = c->edge.npart + c->mid.npart;
     CK(hipMalloc(&c->partial_all, sizeof(double) * std::max(1, c->whole.npart + c->npart_slab)));
     c->whole.part = c->partial_all;
+    {
+      const char* e = std::getenv("LBM_FUSED_RESIDUAL");  // A/B switch: 0 = separate reduction launch
+      c->fuse_red = c->whole.npart > 0 && !(e && e[0] == '0');
+    }
+    if (c->fuse_red) {
+      c->red_n = c->whole.npart + 8;
+      CK(hipMalloc(&c->red_part, sizeof(double) * 2 * c->red_n));
+    }
     c->edge.part = c->whole.part + c->whole.npart;
     c->mid.part = c->edge.part + c->edge.npart;
   }
@@ -662,6 +672,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->bc_in) (void)hipFree(c->bc_in);
   if (c->bc_out) (void)hipFree(c->bc_out);
   if (c->partial_all) (void)hipFree(c->partial_all);
+  if (c->red_part) (void)hipFree(c->red_part);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
   if (c->retried) (void)hipFree(c->retried);
@@ -829,12 +840,25 @@ int rccl_exchange(lbm_ctx* c, int b, bool all) {
 
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
   int h = c->steps_done;
+  if (c->fuse_red && !c->conv_enabled) {
+    // one launch per step: step s's k_step also finishes step s-1's residual; the last
+    // step's own reduction follows the loop
+    const double* prev = nullptr;
+    for (int s = 0; s < nsteps; ++s, ++h) {
+      double* part = c->red_part + (size_t)(s & 1) * c->red_n;
+      const FusedRed fr{part, prev, (want_hist && s > 0) ? c->hist + s - 1 : nullptr};
+      RCK(run_range(c, c->whole, h, s == nsteps - 1, c->s_comp, &fr));
+      prev = part;
+    }
+    HIPCK(c, launch_reduce(prev, c->red_n, c->scratch, c->conv, want_hist ? c->hist + nsteps - 1 : nullptr, 1,
+                           c->s_comp));
+    return LBM_OK;
+  }
   for (int s = 0; s < nsteps; ++s, ++h) {
     const bool store_all = c->conv_enabled || (s == nsteps - 1);
-    MainArgs a{};
-    RCK(run_range(c, c->whole, h, store_all, c->s_comp, true, &a));
+    RCK(run_range(c, c->whole, h, store_all, c->s_comp));
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
-                           1, a.fast_div ? &a : nullptr, c->retried, c->s_comp));
+                           1, c->s_comp));
   }
   return LBM_OK;
 }
@@ -851,14 +875,13 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
     // edge planes first, so their halo travels while the interior runs
-    MainArgs a{};
-    RCK(run_range(c, c->edge, h, store_all, c->s_comp, false));
+    RCK(run_range(c, c->edge, h, store_all, c->s_comp));
     RCK(rccl_exchange(c, (h + 1) & 1, false));
-    RCK(run_range(c, c->mid, h, store_all, c->s_comp, true, &a));
+    RCK(run_range(c, c->mid, h, store_all, c->s_comp));
     // this rank's sum goes to the step-parity slot: the all-reduce of step h - 2, which read
     // the same slot, precedes exchange(h - 1) on s_comm, and s_comp waited for that at the top
-    HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, a.fast_div ? &a : nullptr,
-                           c->retried, c->s_comp, &c->conv->s_slot[h & 1]));
+    HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp,
+                           &c->conv->s_slot[h & 1]));
     HIPCK(c, hipEventRecord(c->ev_sum, c->s_comp));
     HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_sum, 0));
     NCCK(c, ncclAllReduce(&c->conv->s_slot[h & 1], &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
@@ -1163,11 +1186,9 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     const bool store_all = (s == nsteps - 1);
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      MainArgs a{};
-      RCK(run_range(c, c->edge, h, store_all, st, false));
-      RCK(run_range(c, c->mid, h, store_all, st, true, &a));
-      HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, a.fast_div ? &a : nullptr,
-                             c->retried, st));
+      RCK(run_range(c, c->edge, h, store_all, st));
+      RCK(run_range(c, c->mid, h, store_all, st));
+      HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
     }
     RCK(loopback_exchange(cs, n, (h + 1) & 1, false, st));
     hipLaunchKernelGGL(k_sum_locals, dim3(1), dim3(1), 0, st, dconvs, n);

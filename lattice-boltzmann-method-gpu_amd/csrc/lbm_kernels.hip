@@ -21,9 +21,12 @@
 //                        boundary_stream writes into B, ldc.cu:391-456, Poiseulle.cu:748-891,
 //                        bifurcation.cu:877-1021; their hand-simplified "tmp" terms are
 //                        bit-identical to feq_q(rho_bc, u_bc)).
-//  k_reduce_*        deterministic two-level sum of the per-block |u| partials (and any
-//                    chunk the fast division path queued, re-done exactly) and the
-//                    residual / convergence logic of ldc.cu:660-684 on the device.
+//  residual          the |u| partials of a step (one per block) are summed in a fixed order
+//                    by the first block of the NEXT step's launch, which then runs the
+//                    residual / convergence logic of ldc.cu:660-684 on the device, so a step
+//                    is one launch; k_reduce_* do it for the last step of an lbm_step call,
+//                    under convergence control (the stop must be known before the next
+//                    step) and for slabs (the sum goes to the RCCL all-reduce).
 // HBM traffic per fluid cell: 76 B loaded + 76 B stored + 1 B type.
 #include <cmath>
 #include <cstring>
@@ -211,9 +214,10 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
 
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.  NEE-adjacent cells
 // are left to the NEE blocks of the same launch (nee_cell).
-//  FAST: the 3-VALU quotient when the whole wave lies in its domain; a wave that does not
-//        stores nothing and queues its chunk for the exact path, run by the reduction
-//        launch (both paths in one kernel would cost a third of the registers: 232 vs 168).
+//  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
+//        branch) the exact division, counted in exact_waves.  Both paths cost 216 VGPRs
+//        against 170 for one -- no occupancy change, since the LDS reservation already
+//        holds the kernel at two waves per SIMD.
 template <bool FAST, bool SW>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane) {
   double acc = 0.0;
@@ -236,16 +240,15 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   moments<1>(v, r1, x1, y1, z1);
   moments<2>(v, r2, x2, y2, z2);
   moments<3>(v, r3, x3, y3, z3);
+  bool fast_wave = false;
   if constexpr (FAST) {  // non-fluid cells are never stored: they do not constrain the wave
     const unsigned fl = t4 & (t4 >> 1) & 0x01010101u;
     const bool ok = (!(fl & 0x1u) || fast_div_ok<0>(v, x0, y0, z0)) &&
                     (!(fl & 0x100u) || fast_div_ok<1>(v, x1, y1, z1)) &&
                     (!(fl & 0x10000u) || fast_div_ok<2>(v, x2, y2, z2)) &&
                     (!(fl & 0x1000000u) || fast_div_ok<3>(v, x3, y3, z3));
-    if (!__all(ok)) {
-      if (lane == 0) a.retry[atomicAdd(a.retry_count, 1)] = (int)(cb / kChunk);
-      return 0.0;
-    }
+    fast_wave = __all(ok);
+    if (!fast_wave && lane == 0) atomicAdd(a.exact_waves, 1ull);
   }
   // what this lane stores, its |u| terms and (last step) its macros -- all before the
   // relaxation, so that the moments die cell by cell inside it
@@ -286,10 +289,17 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
         }
     }
   }
-  relax_cell<0, FAST>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
-  relax_cell<1, FAST>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
-  relax_cell<2, FAST>(v, a.tau, a.tau_rcp, r2, x2, y2, z2, AllQ{});
-  relax_cell<3, FAST>(v, a.tau, a.tau_rcp, r3, x3, y3, z3, AllQ{});
+  if (FAST && fast_wave) {
+    relax_cell<0, true>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
+    relax_cell<1, true>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
+    relax_cell<2, true>(v, a.tau, a.tau_rcp, r2, x2, y2, z2, AllQ{});
+    relax_cell<3, true>(v, a.tau, a.tau_rcp, r3, x3, y3, z3, AllQ{});
+  } else {  // exact division: tau not verified, or a wave outside the fast quotient's domain
+    relax_cell<0, false>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
+    relax_cell<1, false>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
+    relax_cell<2, false>(v, a.tau, a.tau_rcp, r2, x2, y2, z2, AllQ{});
+    relax_cell<3, false>(v, a.tau, a.tau_rcp, r3, x3, y3, z3, AllQ{});
+  }
   if (t4 & kWall4) {  // rare, divergent: lanes holding wall-adjacent cells
     if (store & 1u) bb_store_cell<0, SW>(a.dst, c, m0, v, a.pitch, a.plane);
     if (store & 2u) bb_store_cell<1, SW>(a.dst, c, m1, v, a.pitch, a.plane);
@@ -542,13 +552,26 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
   double acc = 0.0;
   int slot;
-  if ((int)blockIdx.x >= a.nee_blocks) {
+  const int bx = (int)blockIdx.x - a.red_blocks;
+  if (bx < 0) {  // leading reduction group: block 0 finishes the previous step
+    slot = blockIdx.x;
+    if (blockIdx.x == 0 && a.red_partial != nullptr) {
+      double t = 0.0;
+      for (int i = threadIdx.x; i < a.red_n; i += kBlock) t += a.red_partial[i];  // fixed order
+      t = block_sum(t, red);
+      if (threadIdx.x == 0) {
+        a.red_conv->s_local = t;
+        residual_logic(a.red_conv, t, a.red_hist);
+      }
+      __syncthreads();  // red[] reuse below
+    }
+  } else if (bx >= a.nee_blocks) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own
     // L2), so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of
     // chunks and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
-    const int b = (int)blockIdx.x - a.nee_blocks;  // nee_blocks is a multiple of 8
+    const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
@@ -557,10 +580,10 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     } else if (idx < a.nchunks) {
       acc = process_chunk<FAST, SW>(a, chunk_of(a, idx) * kChunk, lane);  // uniform base
     }
-    slot += a.nee_blocks;
+    slot += a.red_blocks + a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
     slot = blockIdx.x;
-    const int i = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+    const int i = bx * kBlock + (int)threadIdx.x;
     if (i < a.n_nee) acc = nee_cell<SW>(a, i);
   }
   const double s = block_sum(acc, red);
@@ -580,11 +603,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 
 // ---- residual --------------------------------------------------------------------------
 
-// slice b of the block partials -> out[b]; then the chunks the fast path queued, re-done
-// with the exact division by all slice blocks together -> out[gridDim.x + b]
+// slice b of the block partials -> out[b]
 __global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict__ partial, int n,
-                                                       double* __restrict__ out, const ConvState* cv,
-                                                       const MainArgs m, int retry) {
+                                                       double* __restrict__ out, const ConvState* cv) {
   __shared__ double red[4];
   if (cv->stopped) return;
   const int len = (n + gridDim.x - 1) / gridDim.x;
@@ -593,23 +614,10 @@ __global__ __launch_bounds__(256) void k_reduce_slices(const double* __restrict_
   for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s += partial[i];
   s = block_sum(s, red);
   if (threadIdx.x == 0) out[blockIdx.x] = s;
-  double r = 0.0;
-  if (retry) {
-    const int nq = *m.retry_count;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int k = (int)blockIdx.x * 4 + wave; k < nq; k += (int)gridDim.x * 4)
-      r += m.swap ? process_chunk<false, true>(m, (int64_t)m.retry[k] * kChunk, lane)
-                  : process_chunk<false, false>(m, (int64_t)m.retry[k] * kChunk, lane);
-  }
-  __syncthreads();  // red[] reuse
-  r = block_sum(r, red);
-  if (threadIdx.x == 0) out[gridDim.x + blockIdx.x] = r;
 }
 
 __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__ slices, int n, ConvState* cv,
-                                                      double* local_out, float* hist_slot, int finish,
-                                                      int* retry_count, unsigned long long* retried_total) {
+                                                      double* local_out, float* hist_slot, int finish) {
   __shared__ double red[4];
   if (cv->stopped) return;
   double s = 0.0;
@@ -618,48 +626,22 @@ __global__ __launch_bounds__(256) void k_reduce_final(const double* __restrict__
   if (threadIdx.x == 0) {
     *local_out = s;
     if (finish) residual_logic(cv, s, hist_slot);
-    if (retry_count) {
-      const int nq = *retry_count;
-      if (nq) {
-        *retried_total += (unsigned long long)nq;
-        *retry_count = 0;
-      }
-    }
   }
 }
 
-// small launch ranges (n <= kReduceOneMax partials): the whole reduction, retries included,
-// in one block -- one launch less per step where launches dominate (LDC 64^3: ~26 us/step)
+// small launch ranges (n <= kReduceOneMax partials): the whole reduction in one block -- one
+// launch less per step where launches dominate
 constexpr int kReduceOneMax = 16384;
 __global__ __launch_bounds__(512) void k_reduce_one(const double* __restrict__ partial, int n, ConvState* cv,
-                                                     double* local_out, float* hist_slot, int finish,
-                                                     const MainArgs m, int retry,
-                                                     unsigned long long* retried_total) {
+                                                     double* local_out, float* hist_slot, int finish) {
   __shared__ double red[8];
   if (cv->stopped) return;
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];  // fixed order
   s = block_sum(s, red);
-  double r = 0.0;
-  int nq = 0;
-  if (retry) {
-    nq = *m.retry_count;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int k = wave; k < nq; k += (int)(blockDim.x >> 6))
-      r += m.swap ? process_chunk<false, true>(m, (int64_t)m.retry[k] * kChunk, lane)
-                  : process_chunk<false, false>(m, (int64_t)m.retry[k] * kChunk, lane);
-  }
-  __syncthreads();  // red[] reuse
-  r = block_sum(r, red);
   if (threadIdx.x == 0) {
-    s += r;
     *local_out = s;
     if (finish) residual_logic(cv, s, hist_slot);
-    if (nq) {
-      *retried_total += (unsigned long long)nq;
-      *m.retry_count = 0;
-    }
   }
 }
 
@@ -1034,7 +1016,7 @@ int nee_grid(int n) { return (n + 8 * kBlock - 1) / (8 * kBlock) * 8; }
 constexpr size_t kOccupancyLds = 56 * 1024;
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s) {
-  const dim3 grid(a.main_blocks + a.nee_blocks);
+  const dim3 grid(a.red_blocks + a.main_blocks + a.nee_blocks);
   typedef void (*Kern)(const MainArgs);
   const bool sw = a.swap != 0;
   Kern k;
@@ -1052,20 +1034,15 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot, int finish,
-                         const MainArgs* retry, unsigned long long* retried_total, hipStream_t s,
-                         double* local_out) {
+                         hipStream_t s, double* local_out) {
   if (!local_out) local_out = &conv->s_local;
-  MainArgs m{};
-  if (retry) m = *retry;
-  const int do_retry = (retry && retry->retry_count) ? 1 : 0;
   if (n <= kReduceOneMax) {
-    hipLaunchKernelGGL(k_reduce_one, dim3(1), dim3(512), 0, s, partial, n, conv, local_out, hist_slot, finish, m,
-                       do_retry, retried_total);
+    hipLaunchKernelGGL(k_reduce_one, dim3(1), dim3(512), 0, s, partial, n, conv, local_out, hist_slot, finish);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv, m, do_retry);
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, 2 * kReduceBlocks, conv, local_out, hist_slot,
-                     finish, do_retry ? retry->retry_count : nullptr, retried_total);
+  hipLaunchKernelGGL(k_reduce_slices, dim3(kReduceBlocks), dim3(256), 0, s, partial, n, scratch, conv);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(256), 0, s, scratch, kReduceBlocks, conv, local_out, hist_slot,
+                     finish);
   return hipGetLastError();
 }
 

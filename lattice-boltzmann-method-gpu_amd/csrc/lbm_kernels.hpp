@@ -50,7 +50,7 @@ struct Layout {
 //    wavefront per active 256-cell chunk, every neighbour a plain pull, wall bounce-back
 //    stored producer-side; stores every fluid cell of the range except the NEE-adjacent
 //    ones -- disjoint cells, so both parts run concurrently.
-// Partials: one fp64 |u| sum per block (NEE blocks first).
+// Partials: one fp64 |u| sum per block (reduction blocks, NEE blocks, then chunk blocks).
 struct MainArgs {
   const float* src;     // base (past the guard chunk)
   float* dst;
@@ -72,12 +72,11 @@ struct MainArgs {
                         // outside them are not touched
   float tau;
   float tau_rcp;        // RN(1 / tau)
-  int fast_div;         // 1: the chunk path uses the 3-VALU quotient (tau passed
-                        // verify_fast_div), queueing waves outside its domain for a retry
-  int tau_fast;         // 1: tau passed verify_fast_div -- the one-cell paths (NEE cells,
-                        // one cell per lane) use the fast quotient wave by wave, else exact
-  int* retry;           // fast_div: chunks whose wave left the fast quotient's domain ...
-  int* retry_count;     // ... and their count (re-done exactly by the reduction launch)
+  int fast_div;         // 1: tau passed verify_fast_div -- the 3-VALU correctly rounded
+                        // quotient, wave by wave where the populations lie in its domain
+                        // (else the exact division)
+  int tau_fast;         // the same for the one-cell paths (NEE cells, one cell per lane)
+  unsigned long long* exact_waves;  // counts 4-cell waves that fell back to the exact division
   int store_all_macros;
   const int* stopped;   // nullable
   // NEE-adjacent fluid cells
@@ -90,6 +89,15 @@ struct MainArgs {
   int nee_active;       // 0 at step 0: NEE cells are pulled raw (boundary_stream has not run)
   float omc;            // the reference's (1.0f - 1.0f / tau)
   int swap;             // 1: storage rows run along physical y (Layout::swap)
+  // The previous step's residual inside this launch (single domain, one cell per lane, no
+  // convergence control): red_blocks (0 or 8) extra blocks lead the grid; the first sums
+  // red_partial[0 .. red_n) -- the partials of the previous step's launch, complete at this
+  // launch's start -- and runs the residual logic, so a step is one launch, not two.
+  int red_blocks;
+  const double* red_partial;
+  int red_n;
+  struct ConvState* red_conv;
+  float* red_hist;      // nullable: the previous step's history slot
 };
 
 // True when k_step's fast quotient (q0 = x*y, q = fma(fma(-q0, tau, x), y, q0),
@@ -118,13 +126,11 @@ int main_grid(int nchunks, bool quarter);
 constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
 int nee_grid(int n);
 constexpr int kReduceBlocks = 256;
-// partial sums -> conv->s_local (deterministic two-level tree: kReduceBlocks blocks sum
-// fixed contiguous slices into scratch, one block sums scratch); finish=1 also runs the
-// residual logic and writes *hist_slot.  retry (nullable): the step's arguments whose
-// fast_div queue the slice blocks first re-do with the exact division (their |u| sums join
-// the tree); the final block empties the queue and counts it into *retried_total.
+// partial sums -> conv->s_local (deterministic: one block for up to 16384 partials, else
+// kReduceBlocks blocks sum fixed contiguous slices into scratch and one block sums those);
+// finish = 1 also runs the residual logic and writes *hist_slot.
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot,
-                         int finish, const MainArgs* retry, unsigned long long* retried_total, hipStream_t s,
+                         int finish, hipStream_t s,
                          double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
 

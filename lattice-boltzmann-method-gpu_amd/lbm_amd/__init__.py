@@ -434,7 +434,7 @@ class Lattice:
         return {"row_axis": ra.value, "pitch": pitch.value, "x_align": xa.value, "active_chunks": nch.value}
 
     def numerics(self):
-        """(fast_div in use, chunks re-done on the exact division path since creation)."""
+        """(fast_div in use, chunk waves that took the exact division since creation)."""
         fd, n = C.c_int(), C.c_int64()
         self._ck(lbm_lib().lbm_get_numerics(self.h, C.byref(fd), C.byref(n)), "lbm_get_numerics")
         return {"fast_div": bool(fd.value), "retried_chunks": n.value}

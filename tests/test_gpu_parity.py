@@ -58,8 +58,8 @@ def test_ldc_bitwise(gpu, oracle, n, steps, cells_per_lane, row_axis):
 @pytest.mark.parametrize("axis", ["x", "y"])
 def test_fast_division_domain_retry(gpu, oracle, monkeypatch, axis):
     """Populations outside the fast quotient's proven domain (a tiny f, a huge f) make their
-    waves re-run on the exact-division path in the same step: still bit-identical, and the
-    re-done chunks are counted.  Cells chosen next to the lid (NEE fix-up) and a wall."""
+    waves take the exact division in the same launch: still bit-identical, and those chunk
+    waves are counted.  Cells chosen next to the lid (NEE fix-up) and a wall."""
     from lbm_amd import cases
     monkeypatch.setenv("LBM_CELLS_PER_LANE", "4")  # the fast division lives on the 4-cell path
     monkeypatch.setenv("LBM_ROW_AXIS", axis)
@@ -281,7 +281,7 @@ def test_matches_committed_golden(gpu, name):
 
 def test_fast_division_retry_large(gpu, oracle):
     """The same injected out-of-domain populations on LDC 256^3, where the per-block partials
-    exceed the one-block reduction and the re-done chunks go through the sliced reduction."""
+    exceed the one-block reduction (the sliced reduction finishes the last step)."""
     from lbm_amd import cases
     n = 256
     lat, geo = cases.ldc(n)
