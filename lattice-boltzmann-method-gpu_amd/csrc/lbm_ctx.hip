@@ -44,7 +44,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
-  int main_blocks = 0, nee_blocks = 0;
+  int main_blocks = 0, nee_blocks = 0, nee_waves = 4;
   bool quarter = false;   // one cell per lane (small ranges)
 };
 }  // namespace
@@ -264,6 +264,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, c
   a.store_all_macros = store_all ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
   a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
+  a.nee_waves = r.nee_waves;
   a.nee_active = hstep == 0 ? 0 : 1;
   a.omc = c->omc;
   a.swap = c->L.swap;
@@ -305,6 +306,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   };
   scan(lo, hi);
   if (hi2 > lo2) scan(lo2, hi2);
+  double contig = 1.0;
   r.nchunks = (int)chunks.size();
   r.chunk0 = chunks.empty() ? -1 : chunks[0];
   for (size_t i = 1; i < chunks.size() && r.chunk0 >= 0; ++i)
@@ -357,6 +359,9 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       snm[i] = nm[perm[i]];
     }
     HIPCK(c, hipMemcpy(r.cells, sc.data(), sizeof(int) * r.nslow, hipMemcpyHostToDevice));
+    int64_t adj = 0;  // list neighbours that are storage neighbours (their lanes share lines)
+    for (size_t i = 1; i < sc.size(); ++i) adj += sc[i] == sc[i - 1] + 1;
+    if (sc.size() > 1) contig = (double)adj / (double)(sc.size() - 1);
     nm.swap(snm);
     HIPCK(c, hipMalloc(&r.nee_mask, sizeof(uint2) * r.nslow));
     HIPCK(c, hipMemcpy(r.nee_mask, nm.data(), sizeof(uint2) * r.nslow, hipMemcpyHostToDevice));
@@ -366,7 +371,8 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     r.quarter = e ? (e[0] == '1') : (r.nchunks <= kQuarterMaxChunks);
   }
   r.main_blocks = main_grid(r.nchunks, r.quarter);
-  r.nee_blocks = nee_grid(r.nslow);
+  r.nee_waves = nee_waves_for(r.nslow, contig);
+  r.nee_blocks = nee_grid(r.nslow, r.nee_waves);
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }

@@ -583,8 +583,9 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     slot += a.red_blocks + a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
     slot = blockIdx.x;
-    const int i = bx * kBlock + (int)threadIdx.x;
-    if (i < a.n_nee) acc = nee_cell<SW>(a, i);
+    const int w = (int)threadIdx.x >> 6;
+    const int i = (bx * a.nee_waves + w) * 64 + ((int)threadIdx.x & 63);
+    if (w < a.nee_waves && i < a.n_nee) acc = nee_cell<SW>(a, i);
   }
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[slot] = s;
@@ -1008,7 +1009,8 @@ int main_grid(int nchunks, bool quarter) {
   return nchunks ? std::max(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
 }
 // NEE blocks of k_step (first in the grid): a multiple of 8 so the chunk blocks keep their XCD
-int nee_grid(int n) { return (n + 8 * kBlock - 1) / (8 * kBlock) * 8; }
+int nee_waves_for(int n, double contiguous) { return (n <= 16384 && contiguous < 0.5) ? 1 : kBlock / 64; }
+int nee_grid(int n, int waves) { return (n + 8 * 64 * waves - 1) / (8 * 64 * waves) * 8; }
 
 // Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one):
 // a 56-KB dynamic LDS reservation caps every CU at two of these 4-wave blocks whatever the

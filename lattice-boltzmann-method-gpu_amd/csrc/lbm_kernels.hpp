@@ -86,6 +86,8 @@ struct MainArgs {
                           // (face match), y bit q when that cell is a pressure boundary
   int n_nee;
   int nee_blocks;       // multiple of 8 (keeps the chunk blocks' XCD order)
+  int nee_waves;        // active waves per NEE block (1 for short lists: a cell's loads are
+                        // scattered lines, so spreading the waves over more CUs' load pipes pays)
   int nee_active;       // 0 at step 0: NEE cells are pulled raw (boundary_stream has not run)
   float omc;            // the reference's (1.0f - 1.0f / tau)
   int swap;             // 1: storage rows run along physical y (Layout::swap)
@@ -124,7 +126,10 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
 int main_grid(int nchunks, bool quarter);
 constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
-int nee_grid(int n);
+// 1 active wave per NEE block for short, scattered lists (contiguous = fraction of list
+// neighbours that are storage neighbours: their lanes share lines), else 4
+int nee_waves_for(int n, double contiguous);
+int nee_grid(int n, int waves);
 constexpr int kReduceBlocks = 256;
 // partial sums -> conv->s_local (deterministic: one block for up to 16384 partials, else
 // kReduceBlocks blocks sum fixed contiguous slices into scratch and one block sums those);
