@@ -42,6 +42,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int nslow = 0;
   float4* prev = nullptr; // their (rho, u) of the previous step
   uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
+  float4* nee_bc = nullptr;   // their first kNeeSlots NEE neighbours' boundary data (static)
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
   int main_blocks = 0, nee_blocks = 0, nee_waves = 4;
@@ -263,7 +264,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, c
   a.exact_waves = c->retried;
   a.store_all_macros = store_all ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
-  a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
+  a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.nee_bc = r.nee_bc; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
   a.nee_waves = r.nee_waves;
   a.nee_active = hstep == 0 ? 0 : 1;
   a.omc = c->omc;
@@ -365,6 +366,11 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     nm.swap(snm);
     HIPCK(c, hipMalloc(&r.nee_mask, sizeof(uint2) * r.nslow));
     HIPCK(c, hipMemcpy(r.nee_mask, nm.data(), sizeof(uint2) * r.nslow, hipMemcpyHostToDevice));
+    // the boundary cells' data is written by classification and never changes afterwards
+    HIPCK(c, hipMalloc(&r.nee_bc, sizeof(float4) * kNeeSlots * r.nslow));
+    HIPCK(c, launch_nee_gather(r.cells, r.nee_mask, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.nslow, c->L.pitch,
+                               c->L.plane, c->L.swap, c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   {
     const char* e = std::getenv("LBM_CELLS_PER_LANE");  // A/B switch: 1 or 4 (default: by size)
@@ -382,6 +388,7 @@ void free_range(Range& r) {
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
   if (r.nee_mask) (void)hipFree(r.nee_mask);
+  if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
 }
 

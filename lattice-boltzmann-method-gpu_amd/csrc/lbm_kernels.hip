@@ -336,7 +336,6 @@ struct Macro {
 //          cell's own (rho, u) of the previous step.
 // A cell beside one flat face has 5 NEE directions; cells with more (edges, corners of
 // several boundary faces) load the rest where they are used.
-constexpr int kNeeSlots = 5;
 
 template <bool SW>
 __device__ __forceinline__ int64_t cell_off_rt(int q, int pitch, int64_t plane) {
@@ -352,6 +351,7 @@ template <bool SW>
 __device__ __forceinline__ NeeSlot nee_load(const MainArgs& a, int64_t c, int64_t nb, int q) {
   return NeeSlot{a.src[aidx(c, q)], a.rho[nb], a.ux[nb], a.uy[nb], a.uz[nb]};
 }
+__device__ __forceinline__ NeeSlot nee_slot(float own, const float4 b) { return NeeSlot{own, b.x, b.y, b.z, b.w}; }
 
 // the NEE value of direction Q from its slot
 template <int Q>
@@ -404,7 +404,7 @@ __device__ __forceinline__ void nee_put(float* f, const float* nv, const MainArg
 
 template <bool SW, int... Qs>
 __device__ __forceinline__ void nee_pull_all(float* f, const MainArgs& a, int64_t c, const Macro& mp, uint2 m,
-                                             std::integer_sequence<int, Qs...>) {
+                                             const float4* bc, std::integer_sequence<int, Qs...>) {
   const uint32_t nee = a.nee_active ? m.x : 0u;
   NeeSlot sl[kNeeSlots];
   int qs[kNeeSlots];
@@ -416,7 +416,7 @@ __device__ __forceinline__ void nee_pull_all(float* f, const MainArgs& a, int64_
       const int q = __builtin_ctz(rest);
       rest &= rest - 1u;
       qs[j] = q;
-      sl[j] = nee_load<SW>(a, c, c - cell_off_rt<SW>(q, a.pitch, a.plane), q);
+      sl[j] = nee_slot(a.src[aidx(c, q)], bc[j]);
     }
   }
   ((f[Qs] = a.src[aidx(c - cell_off<Qs, SW>(a.pitch, a.plane), Qs)]), ...);
@@ -477,9 +477,13 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const int64_t c = a.cells[i];
   const float4 pv = a.prev[i];
   const Macro mp{pv.x, pv.y, pv.z, pv.w};
+  const uint2 mk = a.nee_mask[i];
+  float4 bc[kNeeSlots];  // static boundary data: no wait on the cell id
+#pragma unroll
+  for (int j = 0; j < kNeeSlots; ++j) bc[j] = a.nee_bc[(int64_t)i * kNeeSlots + j];
   const uint32_t links = a.links[c];
   float f[kQ];
-  nee_pull_all<SW>(f, a, c, mp, a.nee_mask[i], AllQ{});
+  nee_pull_all<SW>(f, a, c, mp, mk, bc, AllQ{});
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
@@ -1087,6 +1091,37 @@ hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks,
     case 4: hipLaunchKernelGGL((k_probe_copy<2, true, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
     default: hipLaunchKernelGGL((k_probe_copy<4, true, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
   }
+  return hipGetLastError();
+}
+
+template <bool SW>
+__global__ void k_nee_gather(const int* __restrict__ cells, const uint2* __restrict__ mask,
+                             const float* __restrict__ rho, const float* __restrict__ ux,
+                             const float* __restrict__ uy, const float* __restrict__ uz, float4* __restrict__ out,
+                             int n, int pitch, int64_t plane) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = cells[i];
+  uint32_t rest = mask[i].x;
+  for (int j = 0; j < kNeeSlots; ++j) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rest) {
+      const int q = __builtin_ctz(rest);
+      rest &= rest - 1u;
+      const int64_t nb = c - cell_off_rt<SW>(q, pitch, plane);
+      v = make_float4(rho[nb], ux[nb], uy[nb], uz[nb]);
+    }
+    out[(int64_t)i * kNeeSlots + j] = v;
+  }
+}
+
+hipError_t launch_nee_gather(const int* cells, const uint2* mask, const float* rho, const float* ux,
+                             const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
+                             int swap, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g((n + 255) / 256);
+  if (swap) hipLaunchKernelGGL(k_nee_gather<true>, g, dim3(256), 0, s, cells, mask, rho, ux, uy, uz, nee_bc, n, pitch, plane);
+  else hipLaunchKernelGGL(k_nee_gather<false>, g, dim3(256), 0, s, cells, mask, rho, ux, uy, uz, nee_bc, n, pitch, plane);
   return hipGetLastError();
 }
 

@@ -82,6 +82,8 @@ struct MainArgs {
   // NEE-adjacent fluid cells
   const int* cells;     // linear ids
   float4* prev;         // per cell: its (rho, ux, uy, uz) of the previous step
+  const float4* nee_bc;   // per cell, kNeeSlots records: the boundary data (rho_bc or NaN, u_bc)
+                          // of its first NEE directions -- static, so loaded with the cell id
   const uint2* nee_mask;  // per cell: x bit q set when c - e_q is an NEE cell supplying q
                           // (face match), y bit q when that cell is a pressure boundary
   int n_nee;
@@ -124,6 +126,11 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
+constexpr int kNeeSlots = 5;  // NEE directions per cell whose data is gathered (one flat face: 5)
+// nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of mask[i].x
+hipError_t launch_nee_gather(const int* cells, const uint2* mask, const float* rho, const float* ux,
+                             const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
+                             int swap, hipStream_t s);
 int main_grid(int nchunks, bool quarter);
 constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
 // 1 active wave per NEE block for short, scattered lists (contiguous = fraction of list
