@@ -43,18 +43,23 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_CELL = 152    # 19 fp32 loads + 19 fp32 stores per fluid cell update
 
 
-def cpu_baseline(n: int = 256, steps: int = 12):
-    """Serial oracle (reference algorithm restated in C, oracle/) on ONE host core, LDC n^3
-    (the C2 lattice), run as a child process with OMP_NUM_THREADS=1."""
+def cpu_baseline(n: int = 512, steps: int = 1):
+    """Serial oracle (the reference algorithm restated in C, oracle/) pinned to ONE host core
+    (oracle/cpu_baseline.py: sched_setaffinity + OMP_NUM_THREADS=1), run as a child process:
+    `value` = LDC n^3, the bench workload itself, for `steps` steps (~12 s per 512^3 step);
+    `c1` = config C1, LDC 64^3, 200 fixed steps."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1")
     out = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), str(n), str(steps)],
-                         env=env, capture_output=True, text=True, timeout=600, check=True)
+                         env=env, capture_output=True, text=True, timeout=900, check=True)
     r = json.loads(out.stdout.strip().splitlines()[-1])
-    return {"value": round(r["mlups"], 3), "unit": "MLUPS", "cores": 1, "kind": "port",
-            "sample": f"oracle/lbm_oracle.c (serial C port of the reference kernels, fp32, two-phase LDC) "
-                      f"on LDC {n}^3 (config C2 lattice), {steps} steps after 1 warm-up, {r['seconds']:.1f} s, "
-                      f"1 thread (OMP_NUM_THREADS=1), host CPU: {r['cpu']}"}
+    b, c1 = r["bench"], r["c1"]
+    return {"value": round(b["mlups"], 3), "unit": "MLUPS", "cores": 1, "kind": "port",
+            "sample": f"oracle/lbm_oracle.c (serial C port of the reference kernels, fp32, two-phase LDC) on LDC "
+                      f"{n}^3 (the bench workload), {steps} step(s) after set-up, {b['seconds']:.1f} s, pinned to "
+                      f"core {r['core']} (sched_setaffinity, OMP_NUM_THREADS=1), host CPU: {r['cpu']}",
+            "c1": {"mlups": round(c1["mlups"], 3), "workload": "config C1: LDC 64^3, 200 fixed steps",
+                   "seconds": c1["seconds"]}}
 
 
 def pmc_traffic(workload: str):
@@ -77,6 +82,26 @@ def small_case_mlups(n: int, steps: int, dev: int):
     dt = time.perf_counter() - t
     lat.close()
     return round(n ** 3 * steps / dt / 1e6, 1)
+
+
+def c5_one_gpu(dev: int, steps: int = 10):
+    """The C5 lattice (LDC 512 x 512 x 4096, 1.07 G cells, ~187 GB) as ONE domain on one GPU:
+    what the 8-GPU configuration's total work costs a single MI355X."""
+    t = time.perf_counter()
+    lat = cases.ldc_device(512, 512, 4096, device=dev)
+    setup = time.perf_counter() - t
+    lat.step(3, history=False)
+    lat.sync()
+    lat.profile(True)
+    t = time.perf_counter()
+    lat.step(steps, history=False)
+    lat.sync()
+    dt = time.perf_counter() - t
+    st = lat.stats()
+    lat.close()
+    return {"mlups": round(512 * 512 * 4096 * steps / dt / 1e6, 1), "steps": steps,
+            "avg_kernel_ms": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]), 3),
+            "setup_s": round(setup, 1)}
 
 
 def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
@@ -103,11 +128,8 @@ def config_lines(dev: int):
     nl, _ = lbm_amd.index_transform(geo)
     out["poiseuille_128x512x128 (C3)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
     # the same lattice on the x-row layout (lbm_desc.row_axis = 1), for comparison
-    os.environ["LBM_ROW_AXIS"] = "x"
-    try:
+    with lbm_amd.tuned(lbm_amd.TUNE_ROW_AXIS, 1):
         lat, geo = cases.poiseuille(128, 512, 128, device=dev)
-    finally:
-        del os.environ["LBM_ROW_AXIS"]
     out["poiseuille_128x512x128 (C3), x rows"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
     lat, geo, _, _ = cases.bifurcation(1, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
@@ -167,7 +189,13 @@ def main():
     nzg = n * world
     lat = cases.ldc_device(n, n, n, z_offset=rank * n, nz_global=nzg, device=local)
     if world > 1:
+        # a rank whose peer died fails its next wait with LBM_ERR_RCCL (async error poll, or
+        # this limit) and exits non-zero, instead of hanging in a halo receive
+        lbm_amd.tune(lbm_amd.TUNE_SYNC_TIMEOUT_S, 300)
         lat.attach_rccl(ldist.share_unique_id(rank, None, lbm_amd.rccl_unique_id), rank, world)
+    rccl_rank, rccl_ranks = lat.comm_info()
+    if rccl_ranks != world:
+        raise SystemExit(f"rank {rank}: RCCL communicator has {rccl_ranks} ranks, WORLD_SIZE {world}")
     counts = lat.counts()
 
     def barrier():
@@ -190,11 +218,18 @@ def main():
     elapsed = t1 - t0
     kern_ms = st["kernel_ms"]
     main_ms, main_n = st["step_kernel_ms"], max(1, st["step_kernel_launches"])
+    per_step = lambda k: st[k + "_ms"] / args.steps  # noqa: E731
+    mine = [rank, rccl_ranks, per_step("edge"), per_step("interior"), per_step("halo"), per_step("halo_exposed"),
+            elapsed / args.steps * 1e3]
     if world > 1:
         elapsed, kern_ms, main_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms], None)
         n_fluid_total = int(ldist.sum_over_ranks([counts["n_fluid"]], None)[0])
+        every = [None] * world
+        dist.all_gather_object(every, mine)
     else:
         n_fluid_total = counts["n_fluid"]
+        every = [mine]
+    parity_ms = [round(st[f"step_kernel_src{b}_ms"] / max(1, st[f"step_kernel_src{b}_launches"]), 4) for b in (0, 1)]
     lat.close()
 
     # attainable streaming bandwidth of this device, same run (context for roofline.frac:
@@ -264,12 +299,27 @@ def main():
                             "on this GPU in this run",
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
+        "step_kernel_ms_by_source_buffer": parity_ms,
         "residual_last": state["residual"],
     }
+    if world > 1:
+        # per-rank slab timings (HIP events, ms per step): edge-plane launch, interior launch,
+        # halo exchange on the communication stream, and the part of the halo that outlasted
+        # the interior launch (not hidden)
+        ranks = [{"rank": r[0], "rccl_ranks": r[1], "edge_ms": round(r[2], 4), "interior_ms": round(r[3], 4),
+                  "halo_ms": round(r[4], 4), "halo_exposed_ms": round(r[5], 4), "wall_ms_per_step": round(r[6], 4)}
+                 for r in sorted(every)]
+        halo = sum(r["halo_ms"] for r in ranks)
+        line["multi_gpu"] = {
+            "rccl_ranks": min(r["rccl_ranks"] for r in ranks),
+            "halo_hidden_frac": round(1.0 - sum(r["halo_exposed_ms"] for r in ranks) / halo, 4) if halo > 0 else None,
+            "per_rank": ranks,
+        }
     if world == 1 and not args.no_secondary:
         line["secondary"] = {"ldc64_mlups (published config)": small_case_mlups(64, 2000, local),
                              "ldc256_mlups (config C2)": small_case_mlups(256, 200, local),
                              f"ldc{n}_random_velocity_start": perturbed_mlups(n, 50, local),
+                             "ldc512x512x4096_one_gpu (C5 lattice, single domain)": c5_one_gpu(local),
                              **config_lines(local)}
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

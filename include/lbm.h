@@ -132,6 +132,25 @@ typedef struct {
 const char* lbm_version(void);
 const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error */
 
+/* Process-wide tuning knobs (not a reference interface: A/B measurement and test switches;
+ * the defaults are the measured best).  Read when a context is created (ROW_AXIS,
+ * CELLS_PER_LANE, EXACT_DIV, FUSED_RESIDUAL, BUFFER_ALLOC).  Returns the previous value, or
+ * LBM_ERR_ARG for an unknown knob / value.  Results are bit-identical for every setting. */
+typedef enum {
+  LBM_TUNE_ROW_AXIS = 0,        /* stands in for lbm_desc.row_axis = 0: 0 choose, 1 x, 2 y */
+  LBM_TUNE_CELLS_PER_LANE = 1,  /* step kernel: 0 by size, 1 one cell per lane, 4 four */
+  LBM_TUNE_EXACT_DIV = 2,       /* 1: the compiler's division by tau everywhere */
+  LBM_TUNE_FUSED_RESIDUAL = 3,  /* 1 (default): the residual rides in the next step's launch */
+  LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 two allocations, 1 one, 2 reversed */
+  LBM_TUNE_SYNC_TIMEOUT_S = 5,  /* RCCL contexts: a wait (lbm_sync, synchronising lbm_step, read-
+                                   outs) longer than this many seconds aborts the communicator
+                                   and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
+                                   asynchronous RCCL error always aborts promptly. */
+  LBM_TUNE_BUFFER_GAP_KB = 6,   /* BUFFER_ALLOC 1: extra KiB between the two buffers */
+  LBM_TUNE_COUNT = 7
+} lbm_tune_knob;
+int lbm_tune(int knob, int value);
+
 /* Lifecycle */
 int lbm_create(const lbm_desc* desc, lbm_ctx** out);
 void lbm_destroy(lbm_ctx* ctx);
@@ -161,11 +180,23 @@ int lbm_set_convergence(lbm_ctx* ctx, int enabled, int max_it, int stag_max, flo
 int lbm_step(lbm_ctx* ctx, int nsteps, float* residual_hist, int* steps_done);
 int lbm_sync(lbm_ctx* ctx);
 
-/* Convergence state: k (steps executed), tol_count, stopped flag, last residual, last S. */
+/* Convergence state: k (steps executed), tol_count, stopped flag (1 converged / max_it,
+ * 2 stopped because the |u| sum became non-finite), last residual, last S. */
 int lbm_get_state(lbm_ctx* ctx, int* k, int* tol_count, int* stopped, float* residual, double* velsum);
+/* NaN guard: *k = the first step whose |u| sum was not finite (0: none so far).  Recorded with
+ * or without convergence control; under convergence control the run also stops there. */
+int lbm_get_nonfinite(lbm_ctx* ctx, int* k);
 
-/* Macroscopic fields of the last step, raster nx*ny*nz; 0 off-fluid (nullable outputs). */
+/* Macroscopic fields of the last step, raster nx*ny*nz; 0 off-fluid (nullable outputs).  The
+ * step kernels store no macros: the first read-out after stepping recomputes them on the
+ * device from the last step's source buffer (the same pulls and sums, so the same bits). */
 int lbm_get_macros(lbm_ctx* ctx, float* rho, float* ux, float* uy, float* uz);
+/* Verification digest of the last step's fields, one uint64 per local plane: the wrapping sum
+ * over the plane's fluid cells of a 64-bit hash of (global x, y, z, bits of rho, ux, uy, uz).
+ * Independent of layout and slab decomposition, so the digests of z-slabs of a lattice equal
+ * the matching planes' digests of the single-domain run when the fields are bit-identical --
+ * a size-independent check at lattice sizes whose fields are too large to copy to the host. */
+int lbm_field_digest(lbm_ctx* ctx, uint64_t* plane_digest);
 /* Populations of the last step (the next step's source), SoA [19][nz][ny][nx]; only fluid
  * cells carry reference-defined values. */
 int lbm_get_f(lbm_ctx* ctx, float* f_soa);
@@ -183,8 +214,11 @@ int lbm_get_counts(lbm_ctx* ctx, int64_t* n_box, int64_t* n_fluid, double* algo_
 int lbm_profile(lbm_ctx* ctx, int enabled);
 int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
 /* The same for one kind of launch: kind 0 = the step kernel (k_step: stream-collide with
- * bounce-back and the NEE-adjacent cells, one launch per step and launch range); kind 1 is
- * reserved (0 launches). */
+ * bounce-back and the NEE-adjacent cells, one launch per step and launch range); kinds 1 / 2 =
+ * those of its launches that read population buffer 0 / 1 (the A-B parity); slabs with RCCL:
+ * 3 = the edge-plane launches, 4 = the interior launches, 5 = the halo exchange on the
+ * communication stream (pack, send/recv, unpack), 6 = how long each step's halo outlasted its
+ * interior launch (clipped at 0: the part of the exchange not hidden; launches = steps). */
 int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
 /* Arithmetic of the relaxation's division by tau (the reference divides, ldc.cu:326-363):
  * fast_div = 1 when the 3-instruction correctly rounded quotient is in use (tau verified
@@ -217,6 +251,8 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs);
  * residual sum. */
 int lbm_rccl_unique_id(uint8_t out_id[128]);
 int lbm_attach_rccl(lbm_ctx* ctx, const uint8_t id[128], int rank, int nranks);
+/* rank and communicator size as RCCL reports them (ncclCommCount); 0 / 1 without RCCL. */
+int lbm_comm_info(lbm_ctx* ctx, int* rank, int* nranks);
 
 /* Single-device loopback decomposition (test and debug path): n contexts, each a z-slab of
  * one lattice on the same device, stepped together with device-to-device halo copies. */

@@ -43,8 +43,9 @@ void lbmh_initial_fields(int case_kind, int nx, int ny, int nz, const int8_t* ge
  * bifurcation.cu:1095-1156 (2).  Returns 0 or < 0 when the file cannot be written. */
 int lbmh_write_vtk(const char* path, int case_kind, int nx, int ny, int nz, const int8_t* geo,
                    const float* ux, const float* uy, const float* uz, float C_U, float CH);
-/* calc_res (bifurcation.cu:1158-1175): sum of |u|^2 over code >= 4 in the output region */
-double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
+/* calc_res (bifurcation.cu:1158-1175): long-double sum of the fp32 |u|^2 over code >= 4 in
+ * the output region */
+long double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
                      const float* uz);
 
 #ifdef __cplusplus

@@ -15,11 +15,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lbm.h"
@@ -30,8 +32,22 @@ using namespace lbm;
 
 namespace {
 std::string g_create_error;
+// process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
+
+// lbm_kernel_times kinds
+enum : int {
+  kKindStep = 0,       // every step-kernel launch
+  kKindSrc0 = 1,       // ... reading population buffer 0
+  kKindSrc1 = 2,       // ... reading buffer 1
+  kKindEdge = 3,       // slab step: the edge-plane launch
+  kKindMid = 4,        // slab step: the interior launch
+  kKindHalo = 5,       // slab step: halo pack -> send/recv -> unpack on the communication stream
+  kKindExposed = 6,    // slab step: halo end after interior end (clipped at 0): the exchange not hidden
+  kKinds = 7
+};
 
 struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) with their work lists
   int64_t c_lo = 0, c_hi = 0, c_lo2 = 0, c_hi2 = 0;
@@ -84,11 +100,21 @@ struct lbm_ctx {
   unsigned long long* retried = nullptr;  // device: 4-cell waves that took the exact division
   // profiling
   bool prof = false;
+  // recorded event pairs, each counted under up to three kinds (lbm_kernel_times)
+  struct Rec {
+    hipEvent_t a, b;
+    int kinds[3];  // -1: unused
+  };
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
-  std::vector<int> ev_kind;   // per recorded pair: 0 stream-collide, 1 boundary fix-up
-  double kernel_ms = 0.0, kind_ms[2] = {0.0, 0.0};
-  int64_t launches = 0, kind_n[2] = {0, 0};
+  std::vector<Rec> recs;
+  hipEvent_t last_mid_end = nullptr;  // the interior launch's end event of the current step
+  double kernel_ms = 0.0, kind_ms[kKinds] = {};
+  int64_t launches = 0, kind_n[kKinds] = {};
+  // lazy macros (k_moments): the step kernels store none; lbm_get_macros recomputes them
+  // from the last step's source buffer when macros_stale
+  bool macros_stale = false;
+  bool last_slab = false;  // the last steps ran the slab ranges (edge + mid), not whole
   // rccl
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -192,10 +218,7 @@ int64_t active_chunks(const lbm_desc& d, int swap) {
 // slabs of a larger lattice and the device-generated cavity keep x unless told otherwise
 int choose_swap(const lbm_desc& d) {
   int axis = d.row_axis;
-  if (axis == 0) {  // A/B and test switch: LBM_ROW_AXIS=x|y stands in for row_axis 0
-    const char* e = std::getenv("LBM_ROW_AXIS");
-    if (e && (e[0] == 'x' || e[0] == 'y')) axis = e[0] == 'x' ? 1 : 2;
-  }
+  if (axis == 0) axis = g_tune[LBM_TUNE_ROW_AXIS];  // A/B and test switch for row_axis 0
   if (axis == 1) return 0;
   if (axis == 2) return 1;
   if ((!d.geo && !d.mask) || (d.nz_global > 0 && d.nz_global != d.nz)) return 0;
@@ -204,38 +227,46 @@ int choose_swap(const lbm_desc& d) {
 }
 
 // time one kernel launch with HIP events on its own stream (lbm_profile)
+int take_event(lbm_ctx* c, hipEvent_t* e) {
+  if (c->ev_pool.size() <= c->ev_used) {
+    hipEvent_t n;
+    HIPCK(c, hipEventCreate(&n));
+    c->ev_pool.push_back(n);
+  }
+  *e = c->ev_pool[c->ev_used++];
+  return LBM_OK;
+}
+
+// bracket launch() with events on st (lbm_profile); counted under kinds k0, k1, k2 (-1: none)
 template <class F>
-int timed(lbm_ctx* c, hipStream_t st, int kind, F&& launch) {
+int timed(lbm_ctx* c, hipStream_t st, int k0, int k1, int k2, F&& launch, hipEvent_t* end_out = nullptr) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof) {
-    while (c->ev_pool.size() < c->ev_used + 2) {
-      hipEvent_t e;
-      HIPCK(c, hipEventCreate(&e));
-      c->ev_pool.push_back(e);
-    }
-    e0 = c->ev_pool[c->ev_used++];
-    e1 = c->ev_pool[c->ev_used++];
-    c->ev_kind.push_back(kind);
+    RCK(take_event(c, &e0));
+    RCK(take_event(c, &e1));
+    c->recs.push_back({e0, e1, {k0, k1, k2}});
     HIPCK(c, hipEventRecord(e0, st));
   }
-  HIPCK(c, launch());
+  RCK(launch());
   if (c->prof) HIPCK(c, hipEventRecord(e1, st));
-  c->launches++;
-  c->kind_n[kind]++;
+  if (end_out) *end_out = e1;
+  for (int k : {k0, k1, k2})
+    if (k >= 0) c->kind_n[k]++;
   return LBM_OK;
 }
 
 int harvest_profile(lbm_ctx* c) {
-  if (c->ev_used == 0) return LBM_OK;
+  if (c->recs.empty()) return LBM_OK;
   HIPCK(c, hipDeviceSynchronize());
-  for (size_t i = 0; i + 1 < c->ev_used; i += 2) {
+  for (const auto& r : c->recs) {
     float ms = 0.f;
-    HIPCK(c, hipEventElapsedTime(&ms, c->ev_pool[i], c->ev_pool[i + 1]));
-    c->kernel_ms += ms;
-    c->kind_ms[c->ev_kind[i / 2]] += ms;
+    HIPCK(c, hipEventElapsedTime(&ms, r.a, r.b));
+    if (r.kinds[0] == kKindStep) c->kernel_ms += ms;
+    for (int k : r.kinds)
+      if (k >= 0) c->kind_ms[k] += (k == kKindExposed ? std::max(0.f, ms) : ms);
   }
   c->ev_used = 0;
-  c->ev_kind.clear();
+  c->recs.clear();
   return LBM_OK;
 }
 
@@ -247,7 +278,7 @@ struct FusedRed {
   float* hist;         // the previous step's history slot (nullable)
 };
 
-int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, const FusedRed* fr = nullptr) {
+int run_range(lbm_ctx* c, Range& r, int hstep, hipStream_t st, const FusedRed* fr = nullptr, int range_kind = -1) {
   MainArgs a{};
   a.src = c->buf[hstep & 1];
   a.dst = c->buf[(hstep + 1) & 1];
@@ -262,7 +293,6 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, c
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
   a.tau_fast = c->fast_div ? 1 : 0;
   a.exact_waves = c->retried;
-  a.store_all_macros = store_all ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
   a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.nee_bc = r.nee_bc; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
   a.nee_waves = r.nee_waves;
@@ -277,7 +307,14 @@ int run_range(lbm_ctx* c, Range& r, int hstep, bool store_all, hipStream_t st, c
     a.red_conv = c->conv;
     a.red_hist = fr->hist;
   }
-  if (r.main_blocks + r.nee_blocks > 0 || fr) RCK(timed(c, st, 0, [&] { return launch_step(a, st); }));
+  if (r.main_blocks + r.nee_blocks > 0 || fr) {
+    c->launches++;
+    RCK(timed(c, st, kKindStep, kKindSrc0 + (hstep & 1), range_kind, [&] {
+                HIPCK(c, launch_step(a, st));
+                return LBM_OK;
+              },
+              range_kind == kKindMid ? &c->last_mid_end : nullptr));
+  }
   return LBM_OK;
 }
 
@@ -373,8 +410,8 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   {
-    const char* e = std::getenv("LBM_CELLS_PER_LANE");  // A/B switch: 1 or 4 (default: by size)
-    r.quarter = e ? (e[0] == '1') : (r.nchunks <= kQuarterMaxChunks);
+    const int cpl = g_tune[LBM_TUNE_CELLS_PER_LANE];  // A/B switch: 1 or 4 (0: by size)
+    r.quarter = cpl ? (cpl == 1) : (r.nchunks <= kQuarterMaxChunks);
   }
   r.main_blocks = main_grid(r.nchunks, r.quarter);
   r.nee_waves = nee_waves_for(r.nslow, contig);
@@ -418,6 +455,7 @@ int reset_state(lbm_ctx* c) {
   }
   c->steps_done = 0;
   c->halo_primed = false;
+  c->macros_stale = false;
   return LBM_OK;
 }
 
@@ -428,6 +466,18 @@ extern "C" {
 const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA wave-chunk stream-collide)"; }
 
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int lbm_tune(int knob, int value) {
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 1 << 20};
+  if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
+      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
+    g_create_error = "lbm_tune: unknown knob or value out of range";
+    return LBM_ERR_ARG;
+  }
+  const int prev = g_tune[knob];
+  g_tune[knob] = value;
+  return prev;
+}
 
 int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   if (!desc || !out) {
@@ -470,10 +520,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   if (c->d.nz_global <= 0) c->d.nz_global = d.nz;
   c->tau = d.tau;
   c->omc = 1.0f - 1.0f / d.tau;  // the reference's (1.0f - 1.0f / tau), evaluated in fp32
-  {
-    const char* ex = std::getenv("LBM_EXACT_DIV");  // A/B switch: force the compiler's division
-    c->fast_div = !(ex && ex[0] == '1') && verify_fast_div(d.tau);
-  }
+  c->fast_div = !g_tune[LBM_TUNE_EXACT_DIV] && verify_fast_div(d.tau);  // A/B: force the compiler's division
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
@@ -511,10 +558,27 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   CK(hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking));
   for (hipEvent_t* e : {&c->ev_edge, &c->ev_halo, &c->ev_sum, &c->ev_fin})
     CK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  for (int b = 0; b < 2; ++b) {
-    CK(hipMalloc(&c->alloc[b], sizeof(float) * L.buf_floats()));
-    c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
-    CK(hipMemsetAsync(c->alloc[b], 0, sizeof(float) * L.buf_floats(), c->s_comp));
+  {
+    // population buffers (lbm_tune LBM_TUNE_BUFFER_ALLOC: 0 two allocations in order, 1 one
+    // allocation holding both at a 2-MiB aligned offset, 2 two allocations, buffer 1 first)
+    const size_t bytes = sizeof(float) * L.buf_floats();
+    const int mode = g_tune[LBM_TUNE_BUFFER_ALLOC];
+    if (mode == 1) {
+      const size_t off = (bytes + (2u << 20) - 1) / (2u << 20) * (2u << 20) +
+                         (size_t)g_tune[LBM_TUNE_BUFFER_GAP_KB] * 1024;
+      CK(hipMalloc(&c->alloc[0], off + bytes));
+      c->alloc[1] = nullptr;
+      c->buf[0] = c->alloc[0] + L.guard * kQ * kChunk;
+      c->buf[1] = reinterpret_cast<float*>(reinterpret_cast<char*>(c->alloc[0]) + off) + L.guard * kQ * kChunk;
+      CK(hipMemsetAsync(c->alloc[0], 0, off + bytes, c->s_comp));
+    } else {
+      for (int k = 0; k < 2; ++k) {
+        const int b = mode == 2 ? 1 - k : k;
+        CK(hipMalloc(&c->alloc[b], bytes));
+        c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
+        CK(hipMemsetAsync(c->alloc[b], 0, bytes, c->s_comp));
+      }
+    }
   }
   CK(hipMalloc(&c->type, L.ncell));
   CK(hipMalloc(&c->links, sizeof(uint32_t) * L.ncell));
@@ -653,10 +717,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     c->npart_slab = c->edge.npart + c->mid.npart;
     CK(hipMalloc(&c->partial_all, sizeof(double) * std::max(1, c->whole.npart + c->npart_slab)));
     c->whole.part = c->partial_all;
-    {
-      const char* e = std::getenv("LBM_FUSED_RESIDUAL");  // A/B switch: 0 = separate reduction launch
-      c->fuse_red = c->whole.npart > 0 && !(e && e[0] == '0');
-    }
+    c->fuse_red = c->whole.npart > 0 && g_tune[LBM_TUNE_FUSED_RESIDUAL] != 0;  // A/B: separate reduction launch
     if (c->fuse_red) {
       c->red_n = c->whole.npart + 8;
       CK(hipMalloc(&c->red_part, sizeof(double) * 2 * c->red_n));
@@ -827,7 +888,7 @@ int unpack_faces(lbm_ctx* c, int b, bool all, bool from_dn, bool from_up, hipStr
   return LBM_OK;
 }
 
-int rccl_exchange(lbm_ctx* c, int b, bool all) {
+int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
   const size_t cnt = (size_t)(all ? kQ : 5) * c->L.plane;
   const int up = c->rank + 1 < c->nranks ? c->rank + 1 : -1;
   const int dn = c->rank > 0 ? c->rank - 1 : -1;
@@ -835,18 +896,21 @@ int rccl_exchange(lbm_ctx* c, int b, bool all) {
   // beside the interior launch
   HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
   HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
-  RCK(pack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
-  NCCK(c, ncclGroupStart());
-  if (up >= 0) {
-    NCCK(c, ncclSend(c->send_up, cnt, ncclFloat, up, c->comm, c->s_comm));
-    NCCK(c, ncclRecv(c->recv_up, cnt, ncclFloat, up, c->comm, c->s_comm));
-  }
-  if (dn >= 0) {
-    NCCK(c, ncclSend(c->send_dn, cnt, ncclFloat, dn, c->comm, c->s_comm));
-    NCCK(c, ncclRecv(c->recv_dn, cnt, ncclFloat, dn, c->comm, c->s_comm));
-  }
-  NCCK(c, ncclGroupEnd());
-  RCK(unpack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
+  RCK(timed(c, c->s_comm, kKindHalo, -1, -1, [&] {
+    RCK(pack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
+    NCCK(c, ncclGroupStart());
+    if (up >= 0) {
+      NCCK(c, ncclSend(c->send_up, cnt, ncclFloat, up, c->comm, c->s_comm));
+      NCCK(c, ncclRecv(c->recv_up, cnt, ncclFloat, up, c->comm, c->s_comm));
+    }
+    if (dn >= 0) {
+      NCCK(c, ncclSend(c->send_dn, cnt, ncclFloat, dn, c->comm, c->s_comm));
+      NCCK(c, ncclRecv(c->recv_dn, cnt, ncclFloat, dn, c->comm, c->s_comm));
+    }
+    NCCK(c, ncclGroupEnd());
+    RCK(unpack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
+    return LBM_OK;
+  }, halo_end));
   HIPCK(c, hipEventRecord(c->ev_halo, c->s_comm));
   return LBM_OK;
 }
@@ -860,7 +924,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     for (int s = 0; s < nsteps; ++s, ++h) {
       double* part = c->red_part + (size_t)(s & 1) * c->red_n;
       const FusedRed fr{part, prev, (want_hist && s > 0) ? c->hist + s - 1 : nullptr};
-      RCK(run_range(c, c->whole, h, s == nsteps - 1, c->s_comp, &fr));
+      RCK(run_range(c, c->whole, h, c->s_comp, &fr));
       prev = part;
     }
     HIPCK(c, launch_reduce(prev, c->red_n, c->scratch, c->conv, want_hist ? c->hist + nsteps - 1 : nullptr, 1,
@@ -868,8 +932,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     return LBM_OK;
   }
   for (int s = 0; s < nsteps; ++s, ++h) {
-    const bool store_all = c->conv_enabled || (s == nsteps - 1);
-    RCK(run_range(c, c->whole, h, store_all, c->s_comp));
+    RCK(run_range(c, c->whole, h, c->s_comp));
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
                            1, c->s_comp));
   }
@@ -884,13 +947,16 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
   }
   int h = c->steps_done;
   for (int s = 0; s < nsteps; ++s, ++h) {
-    const bool store_all = c->conv_enabled || (s == nsteps - 1);
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
     // edge planes first, so their halo travels while the interior runs
-    RCK(run_range(c, c->edge, h, store_all, c->s_comp));
-    RCK(rccl_exchange(c, (h + 1) & 1, false));
-    RCK(run_range(c, c->mid, h, store_all, c->s_comp));
+    RCK(run_range(c, c->edge, h, c->s_comp, nullptr, kKindEdge));
+    hipEvent_t halo_end = nullptr;
+    RCK(rccl_exchange(c, (h + 1) & 1, false, &halo_end));
+    c->last_mid_end = nullptr;
+    RCK(run_range(c, c->mid, h, c->s_comp, nullptr, kKindMid));
+    if (c->prof && halo_end && c->last_mid_end)  // how long the halo outlasts the interior
+      c->recs.push_back({c->last_mid_end, halo_end, {kKindExposed, -1, -1}});
     // this rank's sum goes to the step-parity slot: the all-reduce of step h - 2, which read
     // the same slot, precedes exchange(h - 1) on s_comm, and s_comp waited for that at the top
     HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp,
@@ -903,6 +969,61 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
   }
   HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
   HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));
+  return LBM_OK;
+}
+
+// Wait for both streams.  With an RCCL communicator the wait polls instead of blocking: a
+// peer that failed (ncclCommGetAsyncError) or a wait longer than LBM_TUNE_SYNC_TIMEOUT_S
+// aborts the communicator and returns LBM_ERR_RCCL, so a rank whose neighbour died exits
+// promptly instead of hanging in a halo receive.
+int wait_streams(lbm_ctx* c) {
+  if (!c->comm) {
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comm));
+    return LBM_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const int limit_s = g_tune[LBM_TUNE_SYNC_TIMEOUT_S];
+  for (;;) {
+    const hipError_t a = hipStreamQuery(c->s_comp), b = hipStreamQuery(c->s_comm);
+    if (a == hipSuccess && b == hipSuccess) return LBM_OK;
+    if (a != hipSuccess && a != hipErrorNotReady) HIPCK(c, a);
+    if (b != hipSuccess && b != hipErrorNotReady) HIPCK(c, b);
+    ncclResult_t ar = ncclSuccess;
+    NCCK(c, ncclCommGetAsyncError(c->comm, &ar));
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if ((ar != ncclSuccess && ar != ncclInProgress) || (limit_s > 0 && waited > limit_s)) {
+      c->err = ar != ncclSuccess && ar != ncclInProgress
+                   ? std::string("RCCL peer failure: ") + ncclGetErrorString(ar)
+                   : "RCCL step did not complete within LBM_TUNE_SYNC_TIMEOUT_S = " + std::to_string(limit_s) + " s";
+      (void)ncclCommAbort(c->comm);
+      c->comm = nullptr;
+      return LBM_ERR_RCCL;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(waited < 0.01 ? 20 : 200));
+  }
+}
+
+// lazy macros: the (rho, u) the last step computed, from its source buffer (k_moments) and
+// the NEE-adjacent cells' kept values (k_prev_scatter); steps_done is device-confirmed here
+int refresh_macros(lbm_ctx* c) {
+  HIPCK(c, hipSetDevice(c->d.device));
+  RCK(wait_streams(c));
+  if (!c->macros_stale) return LBM_OK;
+  ConvState h{};
+  HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
+  c->steps_done = h.k;
+  c->macros_stale = false;
+  if (h.k == 0) return LBM_OK;  // no step ran: the initial arrays stand
+  const Layout& L = c->L;
+  const float* src = c->buf[(h.k - 1) & 1];
+  HIPCK(c, launch_moments(src, c->type, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
+                          L.swap, c->s_comp));
+  std::vector<Range*> rs;
+  if (c->last_slab) rs = {&c->edge, &c->mid};
+  else rs = {&c->whole};
+  for (Range* r : rs) HIPCK(c, launch_prev_scatter(r->cells, r->prev, r->nslow, c->rho, c->ux, c->uy, c->uz, c->s_comp));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
   return LBM_OK;
 }
 
@@ -923,10 +1044,11 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
     HIPCK(c, hipMemsetAsync(c->hist, 0xFF, sizeof(float) * nsteps, c->s_comp));  // NaN: step not run
   }
   RCK(c->comm ? step_rccl(c, nsteps, want_hist) : step_single(c, nsteps, want_hist));
+  c->macros_stale = true;
+  c->last_slab = c->comm != nullptr;
   const bool sync = want_hist || steps_done || c->conv_enabled;
   if (sync) {
-    HIPCK(c, hipStreamSynchronize(c->s_comp));
-    HIPCK(c, hipStreamSynchronize(c->s_comm));
+    RCK(wait_streams(c));
     ConvState h{};
     HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
     c->steps_done = h.k;  // device-confirmed (a converged run stops early)
@@ -941,9 +1063,7 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
 int lbm_sync(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
-  HIPCK(c, hipStreamSynchronize(c->s_comp));
-  HIPCK(c, hipStreamSynchronize(c->s_comm));
-  return LBM_OK;
+  return wait_streams(c);
 }
 
 int lbm_get_state(lbm_ctx* c, int* k, int* tol_count, int* stopped, float* residual, double* velsum) {
@@ -953,15 +1073,24 @@ int lbm_get_state(lbm_ctx* c, int* k, int* tol_count, int* stopped, float* resid
   HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
   if (k) *k = h.k;
   if (tol_count) *tol_count = h.tol_count;
-  if (stopped) *stopped = h.stopped;
+  if (stopped) *stopped = h.stopped;  // 2: stopped on a non-finite |u| sum
   if (residual) *residual = h.residual;
   if (velsum) *velsum = c->comm ? h.s_global : h.s_local;
   return LBM_OK;
 }
 
+int lbm_get_nonfinite(lbm_ctx* c, int* k) {
+  if (!c || !k) return LBM_ERR_ARG;
+  RCK(lbm_sync(c));
+  ConvState h{};
+  HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
+  *k = h.nonfinite_k;
+  return LBM_OK;
+}
+
 int lbm_get_macros(lbm_ctx* c, float* rho, float* ux, float* uy, float* uz) {
   if (!c) return LBM_ERR_ARG;
-  RCK(lbm_sync(c));
+  RCK(refresh_macros(c));
   const Layout& L = c->L;
   std::vector<uint8_t> t((size_t)L.ncell);
   HIPCK(c, hipMemcpy(t.data(), c->type, L.ncell, hipMemcpyDeviceToHost));
@@ -978,6 +1107,24 @@ int lbm_get_macros(lbm_ctx* c, float* rho, float* ux, float* uy, float* uz) {
           outs[k][((int64_t)z * L.ny + y) * L.nx + x] = ((t[s] & kClassMask) == kFluid) ? h[s] : 0.0f;
         }
   }
+  return LBM_OK;
+}
+
+int lbm_field_digest(lbm_ctx* c, uint64_t* plane_digest) {
+  if (!c || !plane_digest) return LBM_ERR_ARG;
+  RCK(refresh_macros(c));
+  const Layout& L = c->L;
+  unsigned long long* d = nullptr;
+  HIPCK(c, hipMalloc(&d, sizeof(unsigned long long) * L.nz));
+  struct DevFree {
+    void* p;
+    ~DevFree() { (void)hipFree(p); }
+  } guard{d};
+  HIPCK(c, hipMemsetAsync(d, 0, sizeof(unsigned long long) * L.nz, c->s_comp));
+  HIPCK(c, launch_digest(c->type, c->rho, c->ux, c->uy, c->uz, L.nx, L.ny, L.nz, L.pitch, L.xshift, L.plane,
+                         c->d.z_offset, L.swap, d, c->s_comp));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  HIPCK(c, hipMemcpy(plane_digest, d, sizeof(uint64_t) * L.nz, hipMemcpyDeviceToHost));
   return LBM_OK;
 }
 
@@ -1037,13 +1184,15 @@ int lbm_profile(lbm_ctx* c, int enabled) {
   c->prof = enabled != 0;
   c->kernel_ms = 0.0;
   c->launches = 0;
-  c->kind_ms[0] = c->kind_ms[1] = 0.0;
-  c->kind_n[0] = c->kind_n[1] = 0;
+  for (int k = 0; k < kKinds; ++k) {
+    c->kind_ms[k] = 0.0;
+    c->kind_n[k] = 0;
+  }
   return LBM_OK;
 }
 
 int lbm_kernel_times(lbm_ctx* c, int kind, double* ms, int64_t* launches) {
-  if (!c || kind < 0 || kind > 1) return LBM_ERR_ARG;
+  if (!c || kind < 0 || kind >= kKinds) return LBM_ERR_ARG;
   RCK(harvest_profile(c));
   if (ms) *ms = c->kind_ms[kind];
   if (launches) *launches = c->kind_n[kind];
@@ -1110,6 +1259,15 @@ int lbm_rccl_unique_id(uint8_t out_id[128]) {
   }
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
   std::memcpy(out_id, &id, 128);
+  return LBM_OK;
+}
+
+int lbm_comm_info(lbm_ctx* c, int* rank, int* nranks) {
+  if (!c) return LBM_ERR_ARG;
+  int n = 1;
+  if (c->comm) NCCK(c, ncclCommCount(c->comm, &n));
+  if (rank) *rank = c->comm ? c->rank : 0;
+  if (nranks) *nranks = c->comm ? n : 1;
   return LBM_OK;
 }
 
@@ -1186,6 +1344,10 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   }
   ConvState** dconvs = nullptr;
   HIPCK(c0, hipMalloc(&dconvs, sizeof(ConvState*) * n));
+  struct DevFree {  // every return below releases dconvs
+    void* p;
+    ~DevFree() { (void)hipFree(p); }
+  } dconvs_guard{dconvs};
   std::vector<ConvState*> hc(n);
   for (int i = 0; i < n; ++i) hc[i] = cs[i]->conv;
   HIPCK(c0, hipMemcpy(dconvs, hc.data(), sizeof(ConvState*) * n, hipMemcpyHostToDevice));
@@ -1196,11 +1358,10 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   }
   int h = c0->steps_done;
   for (int s = 0; s < nsteps; ++s, ++h) {
-    const bool store_all = (s == nsteps - 1);
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      RCK(run_range(c, c->edge, h, store_all, st));
-      RCK(run_range(c, c->mid, h, store_all, st));
+      RCK(run_range(c, c->edge, h, st));
+      RCK(run_range(c, c->mid, h, st));
       HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
     }
     RCK(loopback_exchange(cs, n, (h + 1) & 1, false, st));
@@ -1209,9 +1370,12 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
       HIPCK(c0, launch_finish_global(cs[i]->conv, (i == 0 && residual_hist) ? c0->hist + s : nullptr, st));
   }
   HIPCK(c0, hipStreamSynchronize(st));
-  for (int i = 0; i < n; ++i) cs[i]->steps_done += nsteps;
+  for (int i = 0; i < n; ++i) {
+    cs[i]->steps_done += nsteps;
+    cs[i]->macros_stale = true;
+    cs[i]->last_slab = true;
+  }
   if (residual_hist && nsteps > 0)
     HIPCK(c0, hipMemcpy(residual_hist, c0->hist, sizeof(float) * nsteps, hipMemcpyDeviceToHost));
-  HIPCK(c0, hipFree(dconvs));
   return LBM_OK;
 }

@@ -253,7 +253,7 @@ int lbmh_write_vtk(const char* path, int case_kind, int nx, int ny, int nz, cons
   return ofs.good() ? 0 : -2;
 }
 
-double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
+long double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
                      const float* uz) {
   const Box b{nx, ny, nz};
   long double s = 0.0L;
@@ -266,7 +266,7 @@ double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux,
           s = s + v;
         }
       }
-  return (double)s;
+  return s;
 }
 
 }  // extern "C"

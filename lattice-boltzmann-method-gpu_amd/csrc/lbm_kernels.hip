@@ -28,6 +28,7 @@
 //                    under convergence control (the stop must be known before the next
 //                    step) and for slabs (the sum goes to the RCCL all-reduce).
 // HBM traffic per fluid cell: 76 B loaded + 76 B stored + 1 B type.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -250,9 +251,10 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     fast_wave = __all(ok);
     if (!fast_wave && lane == 0) atomicAdd(a.exact_waves, 1ull);
   }
-  // what this lane stores, its |u| terms and (last step) its macros -- all before the
-  // relaxation, so that the moments die cell by cell inside it
-  const f4 R{r0, r1, r2, r3}, UX{x0, x1, x2, x3}, UY{y0, y1, y2, y3}, UZ{z0, z1, z2, z3};
+  // what this lane stores and its |u| terms -- before the relaxation, so that the moments
+  // die cell by cell inside it (macros are not stored: lbm_get_macros recomputes them from
+  // the last step's source buffer, k_moments)
+  const f4 UX{x0, x1, x2, x3}, UY{y0, y1, y2, y3}, UZ{z0, z1, z2, z3};
   unsigned store = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -275,20 +277,6 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
   const bool keep_others = special != 0u || !lane_in || (t4 & (kNeedsMac * 0x01010101u));
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
-  if (a.store_all_macros) {
-    if (whole) {
-      *reinterpret_cast<f4*>(a.rho + c) = R;
-      *reinterpret_cast<f4*>(a.ux + c) = UX;
-      *reinterpret_cast<f4*>(a.uy + c) = UY;
-      *reinterpret_cast<f4*>(a.uz + c) = UZ;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (store & (1u << j)) {
-          a.rho[c + j] = R[j]; a.ux[c + j] = UX[j]; a.uy[c + j] = UY[j]; a.uz[c + j] = UZ[j];
-        }
-    }
-  }
   if (FAST && fast_wave) {
     relax_cell<0, true>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
     relax_cell<1, true>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
@@ -492,10 +480,7 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   relax1(f, a, rho, ux, uy, uz);
   fix_store_all<SW>(f, a.dst, c, links, a.pitch, a.plane, AllQ{});
-  a.prev[i] = make_float4(rho, ux, uy, uz);
-  if (a.store_all_macros) {
-    a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
-  }
+  a.prev[i] = make_float4(rho, ux, uy, uz);  // also the cell's macros (read out lazily)
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
@@ -526,9 +511,6 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   relax1(f, a, rho, ux, uy, uz);
   fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
-  if (a.store_all_macros) {
-    a.rho[c] = rho; a.ux[c] = ux; a.uy[c] = uy; a.uz[c] = uz;
-  }
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
@@ -543,6 +525,13 @@ __device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
   cv->k += 1;
   if (residual <= cv->tol) cv->tol_count += 1;
   if (cv->enabled) cv->stopped = !(cv->k <= cv->max_it && cv->tol_count <= cv->stag_max);
+  // NaN guard (not in the reference, whose loop runs a diverged lattice on to max_it): the
+  // first step whose |u| sum is not finite is recorded; under convergence control it also
+  // stops the run (stopped = 2, lbm_get_state)
+  if (!isfinite(S)) {
+    if (cv->nonfinite_k == 0) cv->nonfinite_k = cv->k;
+    if (cv->enabled) cv->stopped = 2;
+  }
   if (hist_slot) *hist_slot = residual;
 }
 
@@ -983,6 +972,78 @@ __global__ void k_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshif
   }
 }
 
+// ---- macros, read out lazily ------------------------------------------------------------
+// The step kernels store no macros.  lbm_get_macros recomputes the last step's (rho, u) of
+// every fluid cell from that step's source buffer, which the step left intact (A-B
+// pattern): the same 19 pulls and the same fp32 sums as process_chunk / process_cell1, so
+// the bits are those the step used.  NEE-adjacent cells pulled NEE values, not raw slots:
+// their macros are the (rho, u) the step kept in the range's prev list (k_prev_scatter).
+template <bool SW>
+__global__ void k_moments(const float* __restrict__ src, const uint8_t* __restrict__ type, float* rho, float* ux,
+                          float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane) {
+  for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t t = type[c];
+    if ((t & kClassMask) != kFluid || (t & kNeedsMac)) continue;
+    float f[kQ];
+    pull1_all<SW>(f, src, c, pitch, plane, AllQ{});
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) r = r + f[q];
+    rho[c] = r;
+    ux[c] = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / r;
+    uy[c] = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / r;
+    uz[c] = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / r;
+  }
+}
+
+__global__ void k_prev_scatter(const int* __restrict__ cells, const float4* __restrict__ prev, int n, float* rho,
+                               float* ux, float* uy, float* uz) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = cells[i];
+  const float4 p = prev[i];
+  rho[c] = p.x; ux[c] = p.y; uy[c] = p.z; uz[c] = p.w;
+}
+
+// ---- field digest ------------------------------------------------------------------------
+// Per local plane: the wrapping 64-bit sum over its fluid cells of a hash of (global x, y, z,
+// the bits of rho, ux, uy, uz).  Addition mod 2^64 is order-free, so the digest depends on
+// the fields and global coordinates only -- not on the layout, the launch shape or how the
+// lattice is cut into slabs.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_digest(const uint8_t* __restrict__ type, const float* __restrict__ rho, const float* __restrict__ ux,
+                         const float* __restrict__ uy, const float* __restrict__ uz, int nx, int ny, int pitch,
+                         int xshift, int64_t plane, int z_offset, int swap, unsigned long long* out) {
+  __shared__ unsigned long long part[4];
+  const int zl = blockIdx.y;  // local plane
+  uint64_t acc = 0;
+  const int n1 = swap ? nx : ny;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (int64_t)pitch * n1;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int s0 = (int)(i % pitch), s1 = (int)(i / pitch);
+    if (s0 >= (swap ? ny : nx)) continue;
+    const int64_t c = s0 - xshift + (int64_t)s1 * pitch + (int64_t)(zl + 1) * plane;
+    if (c < 0 || (type[c] & kClassMask) != kFluid) continue;
+    const int x = swap ? s1 : s0, y = swap ? s0 : s1;
+    const uint64_t key = (uint64_t)x | ((uint64_t)y << 21) | ((uint64_t)(zl + z_offset) << 42);
+    uint64_t h = mix64(key + 0x9e3779b97f4a7c15ull);
+    h = mix64(h ^ __float_as_uint(rho[c]));
+    h = mix64(h ^ ((uint64_t)__float_as_uint(ux[c]) << 32 | __float_as_uint(uy[c])));
+    h = mix64(h ^ __float_as_uint(uz[c]));
+    acc += h;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out + zl, part[0] + part[1] + part[2] + part[3]);
+}
+
 int grid_for(int64_t n, int block) {
   int64_t g = (n + block - 1) / block;
   if (g > 65536) g = 65536;
@@ -1016,20 +1077,16 @@ int main_grid(int nchunks, bool quarter) {
 int nee_waves_for(int n, double contiguous) { return (n <= 16384 && contiguous < 0.5) ? 1 : kBlock / 64; }
 int nee_grid(int n, int waves) { return (n + 8 * 64 * waves - 1) / (8 * 64 * waves) * 8; }
 
-// Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one):
-// a 56-KB dynamic LDS reservation caps every CU at two of these 4-wave blocks whatever the
-// register count the compiler settles on.
-constexpr size_t kOccupancyLds = 56 * 1024;
-
+// Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one);
+// the 4-cell kernel's register count (214 VGPRs, kernel-resource-usage) gives exactly that.
 hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   const dim3 grid(a.red_blocks + a.main_blocks + a.nee_blocks);
   typedef void (*Kern)(const MainArgs);
   const bool sw = a.swap != 0;
   Kern k;
-  size_t lds = kOccupancyLds;
+  const size_t lds = 0;
   if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
     k = sw ? k_step1<true> : k_step1<false>;
-    lds = 0;
   } else if (a.fast_div) {
     k = sw ? k_step<true, true> : k_step<true, false>;
   } else {
@@ -1122,6 +1179,31 @@ hipError_t launch_nee_gather(const int* cells, const uint2* mask, const float* r
   const dim3 g((n + 255) / 256);
   if (swap) hipLaunchKernelGGL(k_nee_gather<true>, g, dim3(256), 0, s, cells, mask, rho, ux, uy, uz, nee_bc, n, pitch, plane);
   else hipLaunchKernelGGL(k_nee_gather<false>, g, dim3(256), 0, s, cells, mask, rho, ux, uy, uz, nee_bc, n, pitch, plane);
+  return hipGetLastError();
+}
+
+hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
+                          int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
+  if (hi <= lo) return hipSuccess;
+  const dim3 g(grid_for(hi - lo, 256));
+  if (swap) hipLaunchKernelGGL(k_moments<true>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
+  else hipLaunchKernelGGL(k_moments<false>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
+  return hipGetLastError();
+}
+
+hipError_t launch_prev_scatter(const int* cells, const float4* prev, int n, float* rho, float* ux, float* uy,
+                               float* uz, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prev_scatter, dim3((n + 255) / 256), dim3(256), 0, s, cells, prev, n, rho, ux, uy, uz);
+  return hipGetLastError();
+}
+
+hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux, const float* uy, const float* uz,
+                         int nx, int ny, int nz, int pitch, int xshift, int64_t plane, int z_offset, int swap,
+                         unsigned long long* out, hipStream_t s) {
+  const int per_plane = std::max(1, std::min(256, (int)(plane / 4096)));
+  hipLaunchKernelGGL(k_digest, dim3(per_plane, nz), dim3(256), 0, s, type, rho, ux, uy, uz, nx, ny, pitch, xshift,
+                     plane, z_offset, swap, out);
   return hipGetLastError();
 }
 

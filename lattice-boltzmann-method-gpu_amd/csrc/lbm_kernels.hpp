@@ -77,7 +77,6 @@ struct MainArgs {
                         // (else the exact division)
   int tau_fast;         // the same for the one-cell paths (NEE cells, one cell per lane)
   unsigned long long* exact_waves;  // counts 4-cell waves that fell back to the exact division
-  int store_all_macros;
   const int* stopped;   // nullable
   // NEE-adjacent fluid cells
   const int* cells;     // linear ids
@@ -122,7 +121,7 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
   int enabled;          // convergence stopping on/off
   int max_it, stag_max;
   float tol;
-  int pad;
+  int nonfinite_k;      // first step whose |u| sum was not finite (0: none)
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
@@ -145,6 +144,17 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
                          int finish, hipStream_t s,
                          double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
+// lazy macros: (rho, u) of the fluid cells in [lo, hi) from the last step's source buffer
+// (NEE-adjacent cells excepted), then those cells' kept (rho, u)
+hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
+                          int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
+// per local plane digest of the fluid (rho, u) bits keyed by global coordinates (lbm_field_digest);
+// out[nz] must be zeroed
+hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux, const float* uy, const float* uz,
+                         int nx, int ny, int nz, int pitch, int xshift, int64_t plane, int z_offset, int swap,
+                         unsigned long long* out, hipStream_t s);
+hipError_t launch_prev_scatter(const int* cells, const float4* prev, int n, float* rho, float* ux, float* uy,
+                               float* uz, hipStream_t s);
 
 // streaming copy of n4 16-B vectors (lbm_probe_stream): `blocks` x 256 threads; shape 0/1
 // grid-stride non-temporal / plain, 2/3 the same with one contiguous region per XCD, 4/5

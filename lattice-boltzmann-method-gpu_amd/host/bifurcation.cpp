@@ -44,6 +44,7 @@ int main(int argc, char** argv) {
   // host copies start as the initial fields (calc_res at i = 0 reads them: bifurcation.cu:1260)
   drv::Timer timer;
   float residual = 0.0f;
+  long double sum1 = 0.0L, sum2 = 0.0L;  // bifurcation.cu:1179
   for (int i = 0; i <= REPEAT;) {
     // run up to the next save step (or the end) in one call
     int next = (i + time_save - 1) / time_save * time_save;
@@ -53,19 +54,23 @@ int main(int argc, char** argv) {
     i += count;
     const int last = i - 1;
     if (last % time_save == 0) {
-      const double sum1 = lbmh_calc_res(NX, NY, NZ, geo.data(), f.ux.data(), f.uy.data(), f.uz.data());
+      sum1 = lbmh_calc_res(NX, NY, NZ, geo.data(), f.ux.data(), f.uy.data(), f.uz.data());
       f.fetch(ctx);
       const float milli = timer.ms();
-      const double sum2 = lbmh_calc_res(NX, NY, NZ, geo.data(), f.ux.data(), f.uy.data(), f.uz.data());
-      residual = (float)(std::fabs(sum1 - sum2) / sum2);
+      sum2 = lbmh_calc_res(NX, NY, NZ, geo.data(), f.ux.data(), f.uy.data(), f.uz.data());
+      residual = (float)(std::fabs(sum1 - sum2) / sum2);  // long double, then float (bifurcation.cu:1269)
       std::fprintf(logfile, "%g\n", residual);
       std::printf("ITERATION # %d, collapse time: %g ms, residual:%g\n", last, milli, residual);
       lbmh_write_vtk((out + "/bif_" + std::to_string(last) + ".vtk").c_str(), 2, NX, NY, NZ, geo.data(), f.ux.data(),
                      f.uy.data(), f.uz.data(), C_U, CH);
     }
   }
-  // write_once (bifurcation.cu:1055-1074): u_y then u_x on the z = NZ/2 plane.  The reference
-  // reads h_uy[-1] for unstored cells (out of bounds); 0 is written for those here.
+  // write_once (bifurcation.cu:1055-1074): u_y then u_x on the z = NZ/2 plane, every stored
+  // cell.  The host arrays are the device's at that point (copied back at every save step,
+  // bifurcation.cu:1262-1265), and the device macro arrays are never uploaded (1225-1232) nor
+  // written off-fluid (only geo == 4 cells, 592-595): stored non-fluid cells -- walls, ghosts,
+  // inlet, outlet -- hold the zeros of fresh device memory, which lbm_get_macros returns for
+  // them.  The reference reads h_uy[-1] for unstored cells (out of bounds); 0 is written there.
   {
     std::vector<int32_t> index(n);
     lbmh_index_transform(NX, NY, NZ, geo.data(), index.data());

@@ -31,6 +31,9 @@ LBM_CASE_LDC, LBM_CASE_POISEUILLE, LBM_CASE_MASK, LBM_CASE_GENERIC = 0, 1, 2, 3
 LBM_FACE_PX, LBM_FACE_NX, LBM_FACE_PY, LBM_FACE_NY, LBM_FACE_PZ, LBM_FACE_NZ = range(6)
 LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_BC_PRESSURE = 0, 1, 2
 LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
+# lbm_tune knobs (include/lbm.h lbm_tune_knob)
+(TUNE_ROW_AXIS, TUNE_CELLS_PER_LANE, TUNE_EXACT_DIV, TUNE_FUSED_RESIDUAL, TUNE_BUFFER_ALLOC,
+ TUNE_SYNC_TIMEOUT_S, TUNE_BUFFER_GAP_KB) = range(7)
 
 # reference per-case constants
 LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55
@@ -79,11 +82,11 @@ class lbm_desc(C.Structure):
 
 # every symbol include/lbm.h and include/lbm_host.h declare (checked by the CPU tests)
 LBM_SYMBOLS = [
-    "lbm_version", "lbm_last_error", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
-    "lbm_init_case", "lbm_set_f", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
+    "lbm_version", "lbm_last_error", "lbm_tune", "lbm_get_nonfinite", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
+    "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
     "lbm_get_layout",
-    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_group_step", "lbm_probe_stream",
+    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream",
 ]
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
@@ -125,7 +128,7 @@ def host_lib() -> C.CDLL:
             "lbmh_initial_fields": (None, [C.c_int, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p, f32p, f32p, f32p]),
             "lbmh_write_vtk": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p,
                                          C.c_float, C.c_float]),
-            "lbmh_calc_res": (C.c_double, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
+            "lbmh_calc_res": (C.c_longdouble, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -143,6 +146,8 @@ def lbm_lib() -> C.CDLL:
         sig = {
             "lbm_version": (C.c_char_p, []),
             "lbm_last_error": (C.c_char_p, [P]),
+            "lbm_tune": (C.c_int, [C.c_int, C.c_int]),
+            "lbm_get_nonfinite": (C.c_int, [P, ip]),
             "lbm_create": (C.c_int, [C.POINTER(lbm_desc), C.POINTER(P)]),
             "lbm_destroy": (None, [P]),
             "lbm_init_equilibrium": (C.c_int, [P, C.c_int, f32p, f32p, f32p, f32p]),
@@ -155,6 +160,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_get_state": (C.c_int, [P, ip, ip, ip, f32p, f64p]),
             "lbm_get_macros": (C.c_int, [P, f32p, f32p, f32p, f32p]),
             "lbm_get_f": (C.c_int, [P, f32p]),
+            "lbm_field_digest": (C.c_int, [P, C.POINTER(C.c_uint64)]),
             "lbm_get_geo": (C.c_int, [P, C.POINTER(C.c_int8)]),
             "lbm_get_counts": (C.c_int, [P, i64p, i64p, f64p]),
             "lbm_profile": (C.c_int, [P, C.c_int]),
@@ -165,6 +171,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_get_layout": (C.c_int, [P, ip, ip, ip, i64p]),
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+            "lbm_comm_info": (C.c_int, [P, ip, ip]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
             "lbm_probe_stream": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p]),
         }
@@ -177,6 +184,29 @@ def lbm_lib() -> C.CDLL:
 
 def version() -> str:
     return lbm_lib().lbm_version().decode()
+
+
+def tune(knob: int, value: int) -> int:
+    """Set a process-wide lbm_tune knob (read at context creation); returns the old value."""
+    prev = lbm_lib().lbm_tune(knob, value)
+    if prev < 0:
+        raise LbmError(f"lbm_tune({knob}, {value}): {lbm_lib().lbm_last_error(None).decode()}")
+    return prev
+
+
+class tuned:
+    """Context manager: `with tuned(TUNE_ROW_AXIS, 1): ...` restores the old value on exit."""
+
+    def __init__(self, knob: int, value: int):
+        self.knob, self.value = knob, value
+
+    def __enter__(self):
+        self.prev = tune(self.knob, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        tune(self.knob, self.prev)
+        return False
 
 
 # ---------------------------------------------------------------------------------------
@@ -405,13 +435,22 @@ class Lattice:
         r, s = C.c_float(), C.c_double()
         self._ck(lbm_lib().lbm_get_state(self.h, C.byref(k), C.byref(tc), C.byref(st), C.byref(r), C.byref(s)),
                  "lbm_get_state")
-        return {"k": k.value, "tol_count": tc.value, "stopped": bool(st.value), "residual": r.value,
-                "velsum": s.value}
+        nf = C.c_int()
+        self._ck(lbm_lib().lbm_get_nonfinite(self.h, C.byref(nf)), "lbm_get_nonfinite")
+        return {"k": k.value, "tol_count": tc.value, "stopped": st.value, "residual": r.value,
+                "velsum": s.value, "nonfinite_k": nf.value}
 
     def macros(self):
         out = [np.zeros(self.shape, np.float32) for _ in range(4)]
         self._ck(lbm_lib().lbm_get_macros(self.h, *[_ptr(a, C.c_float) for a in out]), "lbm_get_macros")
         return tuple(out)
+
+    def digest(self) -> np.ndarray:
+        """Per-plane uint64 digest of the fluid (rho, u) bits keyed by global coordinates
+        (lbm_field_digest): equal for bit-identical fields whatever the slab cut."""
+        a = np.zeros(self.shape[0], np.uint64)
+        self._ck(lbm_lib().lbm_field_digest(self.h, _ptr(a, C.c_uint64)), "lbm_field_digest")
+        return a
 
     def f(self) -> np.ndarray:
         a = np.zeros((19,) + self.shape, np.float32)
@@ -446,11 +485,18 @@ class Lattice:
         ms, n, by = C.c_double(), C.c_int64(), C.c_double()
         self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
         out = {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
-        for kind, name in ((0, "step_kernel"),):
+        for kind, name in ((0, "step_kernel"), (1, "step_kernel_src0"), (2, "step_kernel_src1"), (3, "edge"),
+                           (4, "interior"), (5, "halo"), (6, "halo_exposed")):
             m, k = C.c_double(), C.c_int64()
             self._ck(lbm_lib().lbm_kernel_times(self.h, kind, C.byref(m), C.byref(k)), "lbm_kernel_times")
             out[name + "_ms"], out[name + "_launches"] = m.value, k.value
         return out
+
+    def comm_info(self):
+        """(rank, communicator size) from RCCL (ncclCommCount); (0, 1) without RCCL."""
+        r, n = C.c_int(), C.c_int()
+        self._ck(lbm_lib().lbm_comm_info(self.h, C.byref(r), C.byref(n)), "lbm_comm_info")
+        return r.value, n.value
 
     def attach_rccl(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

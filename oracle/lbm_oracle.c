@@ -34,6 +34,7 @@ struct orc_lbm {
     orc_bc bcs[16];                  /* ORC_GENERIC (tables owned) */
     int nbc;
     float sum_current;               /* ldc.cu:652 sum_current */
+    int residual_fp64;               /* 1: S summed in fp64 (liblbm's sum), not thrust's fp32 */
 };
 
 static inline long cidx(const orc_lbm* o, int x, int y, int z) {
@@ -571,6 +572,18 @@ static void nee_pressure_cell(orc_lbm* o, int x, int y, int z) {
  * over the reference storage order: LDC brick order (8x8x8, ldc.cu:71), otherwise the
  * compact z,y,x order of index_transform.  Cells never written hold 0. */
 float orc_velsum(const orc_lbm* o) {
+    if (o->residual_fp64) {
+        /* liblbm's S: the same fp32 |u| terms accumulated in fp64 over the stored cells (the
+         * off-fluid ones hold 0), rounded to fp32 once -- an accurate summation, the limit
+         * thrust's fp32 tree approaches; the reference's own order is unspecified */
+        double d = 0.0;
+        for (long c = 0; c < o->ncell; c++) {
+            if (o->kind != ORC_LDC && o->geo[c] == 0) continue;
+            float ux = o->ux[c], uy = o->uy[c], uz = o->uz[c];
+            d += (double)sqrtf(ux * ux + uy * uy + uz * uz);
+        }
+        return (float)d;
+    }
     float s = 0.f;
     const int nx = o->nx, ny = o->ny, nz = o->nz;
     if (o->kind == ORC_LDC) {
@@ -709,6 +722,8 @@ void orc_set_f(orc_lbm* o, const float* f) {
 }
 
 long orc_bad_reads(const orc_lbm* o) { return o->bad_reads; }
+
+void orc_set_residual_fp64(orc_lbm* o, int on) { o->residual_fp64 = on ? 1 : 0; }
 
 /* bifurcation.cu:1158-1175 */
 double orc_calc_res_bif(const orc_lbm* o) {

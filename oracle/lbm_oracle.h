@@ -97,6 +97,9 @@ double orc_calc_res_bif(const orc_lbm* o);
 /* the reference's per-step residual sum (thrust::reduce emulated serially in fp32 over the
  * reference storage order, ldc.cu:660-662) of the current macros */
 float orc_velsum(const orc_lbm* o);
+/* residual sum mode: 0 (default) thrust's fp32 sum emulated serially in the reference storage
+ * order; 1 the fp32 |u| terms summed in fp64 (liblbm's S), for stop-step comparisons */
+void orc_set_residual_fp64(orc_lbm* o, int on);
 
 #ifdef __cplusplus
 }

@@ -62,6 +62,7 @@ def lib() -> C.CDLL:
             "orc_bad_reads": (C.c_long, [P]),
             "orc_calc_res_bif": (C.c_double, [P]),
             "orc_velsum": (C.c_float, [P]),
+            "orc_set_residual_fp64": (None, [P, C.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -194,6 +195,10 @@ class Oracle:
 
     def velsum(self) -> float:
         return float(lib().orc_velsum(self.h))
+
+    def residual_fp64(self, on: bool = True) -> None:
+        """Sum |u| in fp64 like liblbm (default: thrust's fp32 sum, serial, storage order)."""
+        lib().orc_set_residual_fp64(self.h, 1 if on else 0)
 
 
 def feq(rho: float, ux: float, uy: float, uz: float) -> np.ndarray:

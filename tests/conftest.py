@@ -38,17 +38,30 @@ def gpu(lbm):
     return lbm
 
 
+@pytest.fixture
+def knob(lbm):
+    """knob(which, value): set an lbm_tune knob for the rest of the test (restored after)."""
+    saved = []
+
+    def set_(which, value):
+        saved.append((which, lbm.tune(which, value)))
+
+    yield set_
+    for which, prev in reversed(saved):
+        lbm.tune(which, prev)
+
+
 @pytest.fixture(params=["4", "1"], ids=["4cells", "1cell"])
-def cells_per_lane(request, monkeypatch):
+def cells_per_lane(request, knob, lbm):
     """Run a parity test through both stream-collide paths: four cells per lane (the
     bandwidth path) and one cell per lane (what small lattices use by default)."""
-    monkeypatch.setenv("LBM_CELLS_PER_LANE", request.param)
+    knob(lbm.TUNE_CELLS_PER_LANE, int(request.param))
     return int(request.param)
 
 
 @pytest.fixture(params=["x", "y"], ids=["xrows", "yrows"])
-def row_axis(request, monkeypatch):
+def row_axis(request, knob, lbm):
     """Run a parity test on both device layouts: rows along x and rows along y
-    (lbm_desc.row_axis; LBM_ROW_AXIS stands in for row_axis = 0)."""
-    monkeypatch.setenv("LBM_ROW_AXIS", request.param)
+    (lbm_desc.row_axis; LBM_TUNE_ROW_AXIS stands in for row_axis = 0)."""
+    knob(lbm.TUNE_ROW_AXIS, 1 if request.param == "x" else 2)
     return request.param

@@ -13,7 +13,7 @@ HEADERS = {
     "lbm.h": os.path.join(PKG, "lib", "liblbm.so"),
     "lbm_host.h": os.path.join(PKG, "lib", "liblbm_host.so"),
 }
-DECL = re.compile(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*\b(lbmh?_[a-z0-9_]+)\s*\(", re.M)
+DECL = re.compile(r"^\s*(?:const\s+)?(?:long\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*\b(lbmh?_[a-z0-9_]+)\s*\(", re.M)
 
 
 def declared(header: str):

@@ -57,3 +57,86 @@ def test_poiseuille_driver(gpu, oracle, tmp_path):
     want = _oracle_vtk(gpu, oracle, geo, 7, str(tmp_path / "o.vtk"), oracle.POISEUILLE, 1.5441, 0.0000655737,
                        tau=0.58)
     assert got == want
+
+
+def _vtk_mask_independent(path_geo, geo, ux, uy, uz, C_U, CH):
+    """bifurcation.cu:1095-1156 outputSave written here from scratch (not lbmh_write_vtk):
+    C++ ostream default formatting (6 significant digits, %g) of u * C_U in fp32."""
+    nz, ny, nx = geo.shape
+    f32 = np.float32
+    lines = ["# vtk DataFile Version 2.0",
+             "<-- LBM flow with UIV acceleration, http://www.bg.ic.ac.uk/research/m.tang/ulis/ -->",
+             "ASCII", "DATASET STRUCTURED_POINTS",
+             f"DIMENSIONS {nx - 2} {ny - 4} {nz - 2}",
+             "SPACING {0:g} {0:g} {0:g}".format(float(f32(CH))),
+             "ORIGIN {:g} {:g} {:g}".format(float(nx // 2) * float(f32(CH)), float(ny // 2) * float(f32(CH)), 0.0),
+             f"POINT_DATA  {(nx - 2) * (ny - 4) * (nz - 2)}",
+             "VECTORS VELOCITY float"]
+    sl = (slice(1, nz - 1), slice(2, ny - 2), slice(1, nx - 1))
+    stored = geo[sl] != 0
+    cu = f32(C_U)
+    vals = np.stack([np.where(stored, (a[sl] * cu).astype(np.float32), 0) for a in (ux, uy, uz)], axis=-1)
+    body = "".join("%g " % v for v in vals.reshape(-1).astype(np.float64))
+    return "\n".join(lines) + "\n" + body
+
+
+def _calc_res_ld(geo, ux, uy, uz):
+    """bifurcation.cu:1158-1175: fp32 |u|^2 terms summed in long double, z, y, x order."""
+    sl = (slice(1, geo.shape[0] - 1), slice(2, geo.shape[1] - 2), slice(1, geo.shape[2] - 1))
+    m = geo[sl] >= 4
+    v = (ux[sl] * ux[sl] + uy[sl] * uy[sl]) + uz[sl] * uz[sl]
+    terms = v[m].astype(np.longdouble)
+    return np.cumsum(terms)[-1] if terms.size else np.longdouble(0)
+
+
+def _cfmt(v) -> str:
+    """printf("%g") of the C library (C++ ostream prints a float the same way): NaN keeps its
+    sign (-nan from the 0 / 0 of an all-zero field, bifurcation.cu:1269 with the shipped bc)."""
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    ctypes.CDLL(None).snprintf(buf, 64, b"%g", ctypes.c_double(float(v)))
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("block", [0, 1])
+def test_bifurcation_driver(gpu, oracle, tmp_path, block):
+    """bin/bifurcation (bifurcation.cu main) on the shipped geo.txt / bc.txt, REPEAT 4400:
+    bif_0.vtk and bif_4400.vtk byte for byte, the calc_res residuals of CONVERGENCE.log and
+    meas1.txt (write_once), all against the oracle's fields rendered by an independent writer."""
+    import shutil
+    from conftest import GOLDEN
+    src = os.path.join(GOLDEN, "bifurcation")
+    for f in ("geo.txt", "bc.txt"):
+        shutil.copy(os.path.join(src, f), tmp_path / f)
+    r = subprocess.run([os.path.join(BIN, "bifurcation"), "--bc-inlet-block", str(block), "--out", "out"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300, check=True)
+    lines = r.stdout.strip().splitlines()
+    assert [x.split(",")[0] for x in lines[:2]] == ["ITERATION # 0", "ITERATION # 4400"]
+    assert re.fullmatch(r"TOTAL RUNNING TIME: [0-9.e+-]+ MILLI SECONDS#LATTICE65820", lines[-1])
+
+    raw = oracle.read_geo_txt(os.path.join(src, "geo.txt"), 64, 83, 32)
+    geo = oracle.geo_mask(raw)
+    _, inl, outl = oracle.read_bc_txt(os.path.join(src, "bc.txt"), geo, block)
+    o = oracle.Oracle(oracle.MASK, geo, 0.55, inlet_uy=inl, outlet_uy=outl)
+    C_U, CH = 0.24159041, 0.000248925
+    fluid = geo == 4
+    # host arrays before the first copy-back: the initial fields (0 on every fluid cell)
+    prev = (np.zeros(geo.shape, np.float32),) * 3
+    residuals = []
+    for k, steps in ((0, 1), (4400, 4400)):
+        o.step(steps)
+        _, ux, uy, uz = o.macros()
+        got = (tmp_path / "out" / f"bif_{k}.vtk").read_text()
+        assert got == _vtk_mask_independent(None, geo, ux, uy, uz, C_U, CH), f"bif_{k}.vtk"
+        s1, s2 = _calc_res_ld(geo, *prev), _calc_res_ld(geo, ux, uy, uz)
+        residuals.append(np.float32(abs(s1 - s2) / s2))
+        prev = (ux, uy, uz)
+    log = (tmp_path / "out" / "CONVERGENCE.log").read_text().strip().splitlines()
+    assert log[:2] == [_cfmt(r) for r in residuals]
+    assert log[2].endswith(" ERROR IS" + _cfmt(residuals[-1]))
+    # write_once: u_y then u_x of the z = NZ/2 plane, every cell (0 where unstored / off-fluid)
+    _, ux, uy, uz = o.macros()
+    z = geo.shape[0] // 2
+    vals = np.concatenate([np.where(fluid[z], uy[z], 0).ravel(), np.where(fluid[z], ux[z], 0).ravel()])
+    want = "".join("%g " % v for v in vals.astype(np.float32).astype(np.float64))
+    assert (tmp_path / "meas1.txt").read_text() == want

@@ -56,13 +56,13 @@ def test_ldc_bitwise(gpu, oracle, n, steps, cells_per_lane, row_axis):
 
 
 @pytest.mark.parametrize("axis", ["x", "y"])
-def test_fast_division_domain_retry(gpu, oracle, monkeypatch, axis):
+def test_fast_division_domain_retry(gpu, oracle, knob, axis):
     """Populations outside the fast quotient's proven domain (a tiny f, a huge f) make their
     waves take the exact division in the same launch: still bit-identical, and those chunk
     waves are counted.  Cells chosen next to the lid (NEE fix-up) and a wall."""
     from lbm_amd import cases
-    monkeypatch.setenv("LBM_CELLS_PER_LANE", "4")  # the fast division lives on the 4-cell path
-    monkeypatch.setenv("LBM_ROW_AXIS", axis)
+    knob(gpu.TUNE_CELLS_PER_LANE, 4)  # the fast division lives on the 4-cell path
+    knob(gpu.TUNE_ROW_AXIS, 1 if axis == "x" else 2)
     n = 32
     lat, geo = cases.ldc(n)
     assert lat.numerics()["fast_div"]
@@ -80,10 +80,10 @@ def test_fast_division_domain_retry(gpu, oracle, monkeypatch, axis):
     assert lat.numerics()["retried_chunks"] >= 3
 
 
-def test_exact_division_switch(gpu, oracle, monkeypatch):
-    """LBM_EXACT_DIV=1 keeps the compiler's division; results are the same bits."""
+def test_exact_division_switch(gpu, oracle, knob):
+    """LBM_TUNE_EXACT_DIV = 1 keeps the compiler's division; results are the same bits."""
     from lbm_amd import cases
-    monkeypatch.setenv("LBM_EXACT_DIV", "1")
+    knob(gpu.TUNE_EXACT_DIV, 1)
     lat, geo = cases.ldc(24)
     assert not lat.numerics()["fast_div"]
     o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
