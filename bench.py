@@ -230,6 +230,7 @@ def main():
         n_fluid_total = counts["n_fluid"]
         every = [mine]
     parity_ms = [round(st[f"step_kernel_src{b}_ms"] / max(1, st[f"step_kernel_src{b}_launches"]), 4) for b in (0, 1)]
+    placement = lat.placement()
     lat.close()
 
     # attainable streaming bandwidth of this device, same run (context for roofline.frac:
@@ -300,6 +301,7 @@ def main():
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
         "step_kernel_ms_by_source_buffer": parity_ms,
+        "buffer_placement": placement,
         "residual_last": state["residual"],
     }
     if world > 1:

@@ -141,12 +141,16 @@ typedef enum {
   LBM_TUNE_CELLS_PER_LANE = 1,  /* step kernel: 0 by size, 1 one cell per lane, 4 four */
   LBM_TUNE_EXACT_DIV = 2,       /* 1: the compiler's division by tau everywhere */
   LBM_TUNE_FUSED_RESIDUAL = 3,  /* 1 (default): the residual rides in the next step's launch */
-  LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 two allocations, 1 one, 2 reversed */
+  LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 (default) the two fastest-writing of up
+                                   to six allocations (lbm_buffer_placement), 1 the first two */
   LBM_TUNE_SYNC_TIMEOUT_S = 5,  /* RCCL contexts: a wait (lbm_sync, synchronising lbm_step, read-
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
                                    asynchronous RCCL error always aborts promptly. */
-  LBM_TUNE_BUFFER_GAP_KB = 6,   /* BUFFER_ALLOC 1: extra KiB between the two buffers */
+  LBM_TUNE_STEPS_PER_LAUNCH = 6, /* 0 (default) and 1: one time step per launch; 2: two per launch
+                                   (k_step2, LDS temporal blocking) wherever allowed (single
+                                   domain, no convergence control, rows a multiple of 64 slots);
+                                   slower at 512^3, kept as the measured LDS-staged alternative */
   LBM_TUNE_COUNT = 7
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
@@ -228,6 +232,13 @@ int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
  * instead (a wave-uniform branch in the same launch); retried_chunks counts those 256-cell
  * chunk waves since creation.  Results are bit-identical either way. */
 int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
+/* Placement of the two population buffers (not a reference interface).  HBM write bandwidth
+ * differs between allocations (~5.5 vs ~6.4 TB/s for 10-GB buffers on MI355X, stable per
+ * allocation); when a buffer is >= 1 GiB and the device has room, lbm_create allocates up to six
+ * candidates, times one full-buffer write sweep of each and keeps the two fastest.  gbs[0..cap)
+ * receives the candidates' rates (GB/s) in allocation order, *n their count (0: buffers under
+ * 1 GiB, not probed), chosen[2] the indices kept.  Nullable outputs. */
+int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen);
 /* The device layout lbm_create chose (lbm_desc.row_axis / x_align resolved): row_axis 1 = x,
  * 2 = y; pitch = row slots; x_align 1..4; active_chunks = 256-cell chunks k_step launches a
  * wave for (those holding fluid).  Nullable outputs. */

@@ -46,7 +46,8 @@ enum : int {
   kKindMid = 4,        // slab step: the interior launch
   kKindHalo = 5,       // slab step: halo pack -> send/recv -> unpack on the communication stream
   kKindExposed = 6,    // slab step: halo end after interior end (clipped at 0): the exchange not hidden
-  kKinds = 7
+  kKindTwoStep = 7,    // k_step2 launches (two time steps each)
+  kKinds = 8
 };
 
 struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) with their work lists
@@ -57,6 +58,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int* cells = nullptr;   // NEE-adjacent fluid cells
   int nslow = 0;
   float4* prev = nullptr; // their (rho, u) of the previous step
+  float4* prev_alt = nullptr;  // k_step2's output copy (swapped with prev after each two-step launch)
   uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
   float4* nee_bc = nullptr;   // their first kNeeSlots NEE neighbours' boundary data (static)
   double* part = nullptr; // main partials, then fix-up partials
@@ -71,8 +73,11 @@ struct lbm_ctx {
   Layout L{};
   hipStream_t s_comp = nullptr, s_comm = nullptr;
   hipEvent_t ev_edge = nullptr, ev_halo = nullptr, ev_sum = nullptr, ev_fin = nullptr;
-  float* alloc[2] = {nullptr, nullptr};
+  float* alloc[2] = {nullptr, nullptr};  // hipMalloc'd population buffers
+  std::vector<double> cand_gbs;           // buffer_placement: candidates' sweep-write rates (GB/s)
+  int chosen[2] = {0, 1};                 // the two candidates kept
   float* buf[2] = {nullptr, nullptr};  // past the guard chunk
+  int cur = 0;                         // buf[cur] holds the current state (every launch flips it)
   uint8_t* type = nullptr;
   uint32_t* links = nullptr;
   int8_t* codes = nullptr;               // reference codes per storage cell (lbm_get_geo)
@@ -114,6 +119,11 @@ struct lbm_ctx {
   // lazy macros (k_moments): the step kernels store none; lbm_get_macros recomputes them
   // from the last step's source buffer when macros_stale
   bool macros_stale = false;
+  bool macros_stored = false;  // the last launch stored (rho, u) itself (k_step2 on a call's last launch)
+  // two steps per launch (k_step2, single domain): per-cell NEE-list index, step t+2 partials
+  int* nee_idx = nullptr;
+  double* part2 = nullptr;
+  int step2_nblk = 0;
   bool last_slab = false;  // the last steps ran the slab ranges (edge + mid), not whole
   // rccl
   ncclComm_t comm = nullptr;
@@ -278,10 +288,27 @@ struct FusedRed {
   float* hist;         // the previous step's history slot (nullable)
 };
 
-int run_range(lbm_ctx* c, Range& r, int hstep, hipStream_t st, const FusedRed* fr = nullptr, int range_kind = -1) {
+void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
+  a.src = c->buf[srcbuf];
+  a.dst = c->buf[srcbuf ^ 1];
+  a.type = c->type; a.links = c->links;
+  a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
+  a.pitch = c->L.pitch; a.plane = c->L.plane;
+  a.tau = c->tau;
+  a.tau_rcp = 1.0f / c->tau;
+  a.tau_fast = c->fast_div ? 1 : 0;
+  a.exact_waves = c->retried;
+  a.omc = c->omc;
+  a.swap = c->L.swap;
+}
+
+// one step of a range from buffer srcbuf into srcbuf ^ 1 (hstep: the step's number, for the
+// raw NEE pulls of step 0)
+int run_range(lbm_ctx* c, Range& r, int hstep, int srcbuf, hipStream_t st, const FusedRed* fr = nullptr,
+              int range_kind = -1) {
   MainArgs a{};
-  a.src = c->buf[hstep & 1];
-  a.dst = c->buf[(hstep + 1) & 1];
+  a.src = c->buf[srcbuf];
+  a.dst = c->buf[srcbuf ^ 1];
   a.type = c->type; a.links = c->links;
   a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
   a.partial = r.part;
@@ -309,7 +336,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, hipStream_t st, const FusedRed* f
   }
   if (r.main_blocks + r.nee_blocks > 0 || fr) {
     c->launches++;
-    RCK(timed(c, st, kKindStep, kKindSrc0 + (hstep & 1), range_kind, [&] {
+    RCK(timed(c, st, kKindStep, kKindSrc0 + srcbuf, range_kind, [&] {
                 HIPCK(c, launch_step(a, st));
                 return LBM_OK;
               },
@@ -424,6 +451,7 @@ void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
+  if (r.prev_alt) (void)hipFree(r.prev_alt);
   if (r.nee_mask) (void)hipFree(r.nee_mask);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
@@ -454,9 +482,85 @@ int reset_state(lbm_ctx* c) {
     HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   c->steps_done = 0;
+  c->cur = 0;
+  c->macros_stored = false;
   c->halo_primed = false;
   c->macros_stale = false;
   return LBM_OK;
+}
+
+// Population buffers: two allocations of `bytes`, picked by measured write rate.
+//
+// HBM write bandwidth is a property of the physical memory an allocation receives: on the pool's
+// MI355X boxes a 10-GB allocation sweep-writes at either ~6.3-6.5 or ~5.5 TB/s, stable for the
+// allocation's lifetime and the same for every sweep order (one region per XCD, grid-stride,
+// reversed or rotated regions), while reads differ by < 4% (tools/place_lab.hip,
+// gpurun_out/r02g-i).  A copy runs at its destination's rate, and k_step writes one buffer per
+// step, so a slow buffer costs every other step ~8% (the 3.4 / 3.7 ms alternation at 512^3).
+// When the device has room (hipMemGetInfo, after `others` bytes for the remaining arrays), up to
+// four extra candidates are allocated, each zeroed and timed over one full-buffer sweep of
+// non-temporal 16-B stores, and the two fastest kept; the rest are freed before any other array
+// is allocated.  Lattices under 1 GiB per buffer (L2 / MALL resident, latency-bound) and
+// LBM_TUNE_BUFFER_ALLOC = 1 take the first two allocations (the latter still timed, for A/B).
+hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
+  constexpr int kMaxCand = 6;
+  int ncand = 2;
+  const bool probe = bytes >= ((size_t)1 << 30);
+  if (!g_tune[LBM_TUNE_BUFFER_ALLOC] && probe) {
+    size_t fr = 0, tot = 0;
+    hipError_t e = hipMemGetInfo(&fr, &tot);
+    if (e != hipSuccess) return e;
+    const size_t need = 2 * bytes + others;
+    if (fr > need) ncand = (int)std::min<size_t>(kMaxCand, 2 + (fr - need) / bytes);
+  }
+  std::vector<float*> p;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < ncand && e == hipSuccess; ++i) {
+    float* q = nullptr;
+    e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) {
+      if (i >= 2) {  // out of room after all: probe what we have
+        (void)hipGetLastError();
+        e = hipSuccess;
+        ncand = i;
+      }
+      break;
+    }
+    p.push_back(q);
+    e = hipMemsetAsync(q, 0, bytes, c->s_comp);
+  }
+  if (e == hipSuccess && probe) {
+    const int64_t n4 = (int64_t)(bytes / 16);
+    e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    for (int i = 0; i < ncand && e == hipSuccess; ++i) {
+      e = launch_probe_fill(p[i], n4, c->s_comp);  // warm-up sweep (the memset's shape differs)
+      if (e == hipSuccess) e = hipEventRecord(e0, c->s_comp);
+      if (e == hipSuccess) e = launch_probe_fill(p[i], n4, c->s_comp);
+      if (e == hipSuccess) e = hipEventRecord(e1, c->s_comp);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      float ms = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      c->cand_gbs.push_back(ms > 0.f ? (double)bytes / (ms * 1e-3) / 1e9 : 0.0);
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (e == hipSuccess && ncand > 2) {
+    std::vector<int> order(ncand);
+    for (int i = 0; i < ncand; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return c->cand_gbs[a] > c->cand_gbs[b]; });
+    c->chosen[0] = std::min(order[0], order[1]);  // keep allocation order between the two
+    c->chosen[1] = std::max(order[0], order[1]);
+  }
+  for (int i = 0; i < (int)p.size(); ++i) {
+    if (e == hipSuccess && (i == c->chosen[0] || i == c->chosen[1]))
+      c->alloc[i == c->chosen[0] ? 0 : 1] = p[i];
+    else
+      (void)hipFree(p[i]);
+  }
+  return e;
 }
 
 }  // namespace
@@ -468,7 +572,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 1 << 20};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 2};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -559,26 +663,11 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   for (hipEvent_t* e : {&c->ev_edge, &c->ev_halo, &c->ev_sum, &c->ev_fin})
     CK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
-    // population buffers (lbm_tune LBM_TUNE_BUFFER_ALLOC: 0 two allocations in order, 1 one
-    // allocation holding both at a 2-MiB aligned offset, 2 two allocations, buffer 1 first)
+    // population buffers (buffer_placement(); LBM_TUNE_BUFFER_ALLOC 1: first two allocations)
     const size_t bytes = sizeof(float) * L.buf_floats();
-    const int mode = g_tune[LBM_TUNE_BUFFER_ALLOC];
-    if (mode == 1) {
-      const size_t off = (bytes + (2u << 20) - 1) / (2u << 20) * (2u << 20) +
-                         (size_t)g_tune[LBM_TUNE_BUFFER_GAP_KB] * 1024;
-      CK(hipMalloc(&c->alloc[0], off + bytes));
-      c->alloc[1] = nullptr;
-      c->buf[0] = c->alloc[0] + L.guard * kQ * kChunk;
-      c->buf[1] = reinterpret_cast<float*>(reinterpret_cast<char*>(c->alloc[0]) + off) + L.guard * kQ * kChunk;
-      CK(hipMemsetAsync(c->alloc[0], 0, off + bytes, c->s_comp));
-    } else {
-      for (int k = 0; k < 2; ++k) {
-        const int b = mode == 2 ? 1 - k : k;
-        CK(hipMalloc(&c->alloc[b], bytes));
-        c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
-        CK(hipMemsetAsync(c->alloc[b], 0, bytes, c->s_comp));
-      }
-    }
+    const size_t others = (size_t)L.ncell * (1 + 4 + 16 + 4) + ((size_t)1 << 30);  // type, links, macros, lists
+    CK(buffer_placement(c, bytes, others));
+    for (int b = 0; b < 2; ++b) c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
   }
   CK(hipMalloc(&c->type, L.ncell));
   CK(hipMalloc(&c->links, sizeof(uint32_t) * L.ncell));
@@ -746,6 +835,8 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->bc_in) (void)hipFree(c->bc_in);
   if (c->bc_out) (void)hipFree(c->bc_out);
   if (c->partial_all) (void)hipFree(c->partial_all);
+  if (c->nee_idx) (void)hipFree(c->nee_idx);
+  if (c->part2) (void)hipFree(c->part2);
   if (c->red_part) (void)hipFree(c->red_part);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
@@ -820,6 +911,17 @@ int lbm_set_f(lbm_ctx* c, const float* f) {
   for (int b = 0; b < 2; ++b)
     HIPCK(c, hipMemcpy(c->buf[b], h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
   return reset_state(c);
+}
+
+int lbm_buffer_placement(lbm_ctx* c, double* gbs, int cap, int* n, int* chosen) {
+  if (!c) return LBM_ERR_ARG;
+  for (int i = 0; gbs && i < cap && i < (int)c->cand_gbs.size(); ++i) gbs[i] = c->cand_gbs[i];
+  if (n) *n = (int)c->cand_gbs.size();
+  if (chosen) {
+    chosen[0] = c->chosen[0];
+    chosen[1] = c->chosen[1];
+  }
+  return LBM_OK;
 }
 
 int lbm_get_numerics(lbm_ctx* c, int* fast_div, int64_t* retried_chunks) {
@@ -915,24 +1017,85 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
   return LBM_OK;
 }
 
+// k_step2 geometry: planes per z run (units = tiles x runs: enough for a few rounds of the
+// 256 CUs, runs long enough that the two pipeline-fill planes per run stay a few percent)
+int step2_zlen(const lbm_ctx* c) {
+  const int64_t tiles = (int64_t)((c->L.pitch + 63) / 64) * ((c->L.plane / c->L.pitch + 5) / 6);
+  const int64_t z = (int64_t)c->L.nz * tiles / 2048;
+  return (int)std::max<int64_t>(16, std::min<int64_t>(64, z));
+}
+
+// two steps per launch (LBM_TUNE_STEPS_PER_LAUNCH = 2): single domain, no convergence control
+// (the stop must be known after every step), rows a multiple of 64 slots.  Opt-in: at 512^3 k_step2 measured 5.07 ms per step
+// against k_step's 3.7 ("Two steps per launch"), so the default is one.
+bool use_step2(const lbm_ctx* c) {
+  return g_tune[LBM_TUNE_STEPS_PER_LAUNCH] == 2 && !c->conv_enabled && !c->comm && c->L.pitch % 64 == 0;
+}
+
+int ensure_step2(lbm_ctx* c) {
+  if (c->nee_idx) return LBM_OK;
+  const int nblk = step2_blocks(c->L.pitch, (int)(c->L.plane / c->L.pitch), c->L.nz, step2_zlen(c));
+  HIPCK(c, hipMalloc(&c->part2, sizeof(double) * 2 * nblk));
+  c->step2_nblk = nblk;
+  HIPCK(c, hipMalloc(&c->nee_idx, sizeof(int) * c->L.ncell));
+  HIPCK(c, hipMemsetAsync(c->nee_idx, 0xFF, sizeof(int) * c->L.ncell, c->s_comp));
+  HIPCK(c, launch_scatter_idx(c->whole.cells, c->whole.nslow, c->nee_idx, c->s_comp));
+  if (c->whole.nslow) HIPCK(c, hipMalloc(&c->whole.prev_alt, sizeof(float4) * c->whole.nslow));
+  return LBM_OK;
+}
+
+// steps h and h + 1 in one k_step2 launch, buf[cur] -> buf[cur ^ 1]; store: the call's last
+// launch, which stores (rho, u) itself (no source buffer of step h + 1 to recompute them from)
+int run_step2(lbm_ctx* c, int h, bool store, float* hist) {
+  MainArgs a{};
+  fill_main_args(c, a, c->cur);
+  a.partial = c->part2;
+  a.nee_active = h == 0 ? 0 : 1;
+  a.prev = c->whole.prev; a.nee_mask = c->whole.nee_mask; a.nee_bc = c->whole.nee_bc;
+  const int nblk = c->step2_nblk;
+  c->launches++;
+  RCK(timed(c, c->s_comp, kKindStep, kKindSrc0 + c->cur, kKindTwoStep, [&] {
+    HIPCK(c, launch_step2(a, c->whole.prev_alt, c->nee_idx, c->part2 + nblk, (int)(c->L.plane / c->L.pitch), c->L.nz,
+                          step2_zlen(c), c->L.ncell, store ? 1 : 0, c->s_comp));
+    return LBM_OK;
+  }));
+  c->cur ^= 1;
+  std::swap(c->whole.prev, c->whole.prev_alt);
+  HIPCK(c, launch_reduce(c->part2, nblk, c->scratch, c->conv, hist, 1, c->s_comp));
+  HIPCK(c, launch_reduce(c->part2 + nblk, nblk, c->scratch, c->conv, hist ? hist + 1 : nullptr, 1, c->s_comp));
+  return LBM_OK;
+}
+
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
   int h = c->steps_done;
+  int s0 = 0;
+  c->macros_stored = false;
+  if (use_step2(c) && nsteps >= 2) {
+    RCK(ensure_step2(c));
+    for (; s0 + 2 <= nsteps; s0 += 2, h += 2) RCK(run_step2(c, h, s0 + 2 == nsteps, want_hist ? c->hist + s0 : nullptr));
+    if (s0 == nsteps) {
+      c->macros_stored = true;
+      return LBM_OK;
+    }
+  }
   if (c->fuse_red && !c->conv_enabled) {
     // one launch per step: step s's k_step also finishes step s-1's residual; the last
     // step's own reduction follows the loop
     const double* prev = nullptr;
-    for (int s = 0; s < nsteps; ++s, ++h) {
+    for (int s = s0; s < nsteps; ++s, ++h) {
       double* part = c->red_part + (size_t)(s & 1) * c->red_n;
-      const FusedRed fr{part, prev, (want_hist && s > 0) ? c->hist + s - 1 : nullptr};
-      RCK(run_range(c, c->whole, h, c->s_comp, &fr));
+      const FusedRed fr{part, prev, (want_hist && s > s0) ? c->hist + s - 1 : nullptr};
+      RCK(run_range(c, c->whole, h, c->cur, c->s_comp, &fr));
+      c->cur ^= 1;
       prev = part;
     }
     HIPCK(c, launch_reduce(prev, c->red_n, c->scratch, c->conv, want_hist ? c->hist + nsteps - 1 : nullptr, 1,
                            c->s_comp));
     return LBM_OK;
   }
-  for (int s = 0; s < nsteps; ++s, ++h) {
-    RCK(run_range(c, c->whole, h, c->s_comp));
+  for (int s = s0; s < nsteps; ++s, ++h) {
+    RCK(run_range(c, c->whole, h, c->cur, c->s_comp));
+    c->cur ^= 1;
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
                            1, c->s_comp));
   }
@@ -942,7 +1105,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
 int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
   RCK(ensure_halo_buffers(c));
   if (!c->halo_primed) {  // ghost planes of the initial source buffer: all 19 populations
-    RCK(rccl_exchange(c, c->steps_done & 1, true));
+    RCK(rccl_exchange(c, c->cur, true));
     c->halo_primed = true;
   }
   int h = c->steps_done;
@@ -950,11 +1113,12 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
     // edge planes first, so their halo travels while the interior runs
-    RCK(run_range(c, c->edge, h, c->s_comp, nullptr, kKindEdge));
+    RCK(run_range(c, c->edge, h, c->cur, c->s_comp, nullptr, kKindEdge));
     hipEvent_t halo_end = nullptr;
-    RCK(rccl_exchange(c, (h + 1) & 1, false, &halo_end));
+    RCK(rccl_exchange(c, c->cur ^ 1, false, &halo_end));
     c->last_mid_end = nullptr;
-    RCK(run_range(c, c->mid, h, c->s_comp, nullptr, kKindMid));
+    RCK(run_range(c, c->mid, h, c->cur, c->s_comp, nullptr, kKindMid));
+    c->cur ^= 1;
     if (c->prof && halo_end && c->last_mid_end)  // how long the halo outlasts the interior
       c->recs.push_back({c->last_mid_end, halo_end, {kKindExposed, -1, -1}});
     // this rank's sum goes to the step-parity slot: the all-reduce of step h - 2, which read
@@ -1014,9 +1178,9 @@ int refresh_macros(lbm_ctx* c) {
   HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
   c->steps_done = h.k;
   c->macros_stale = false;
-  if (h.k == 0) return LBM_OK;  // no step ran: the initial arrays stand
+  if (h.k == 0 || c->macros_stored) return LBM_OK;  // no step ran (initial arrays), or stored by k_step2
   const Layout& L = c->L;
-  const float* src = c->buf[(h.k - 1) & 1];
+  const float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
   HIPCK(c, launch_moments(src, c->type, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
                           L.swap, c->s_comp));
   std::vector<Range*> rs;
@@ -1039,6 +1203,7 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
   }
   HIPCK(c, hipSetDevice(c->d.device));
   const bool want_hist = residual_hist != nullptr;
+  const int k0 = c->steps_done, cur0 = c->cur;
   if (want_hist) {
     RCK(ensure_hist(c, nsteps));
     HIPCK(c, hipMemsetAsync(c->hist, 0xFF, sizeof(float) * nsteps, c->s_comp));  // NaN: step not run
@@ -1052,6 +1217,7 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
     ConvState h{};
     HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
     c->steps_done = h.k;  // device-confirmed (a converged run stops early)
+    if (c->conv_enabled) c->cur = cur0 ^ ((h.k - k0) & 1);  // one step per launch under convergence control
     if (want_hist) HIPCK(c, hipMemcpy(residual_hist, c->hist, sizeof(float) * nsteps, hipMemcpyDeviceToHost));
     if (steps_done) *steps_done = c->steps_done;
   } else {
@@ -1145,7 +1311,7 @@ int lbm_get_f(lbm_ctx* c, float* f) {
   RCK(lbm_sync(c));
   const Layout& L = c->L;
   std::vector<float> h((size_t)L.nchunk * kQ * kChunk);
-  HIPCK(c, hipMemcpy(h.data(), c->buf[c->steps_done & 1], sizeof(float) * h.size(), hipMemcpyDeviceToHost));
+  HIPCK(c, hipMemcpy(h.data(), c->buf[c->cur], sizeof(float) * h.size(), hipMemcpyDeviceToHost));
   for (int q = 0; q < kQ; ++q)
     for (int z = 0; z < L.nz; ++z)
       for (int y = 0; y < L.ny; ++y) {
@@ -1330,7 +1496,7 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   for (int i = 0; i < n; ++i) {
     if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xshift != c0->L.xshift ||
         cs[i]->L.swap != c0->L.swap || cs[i]->L.plane != c0->L.plane ||
-        cs[i]->steps_done != c0->steps_done || cs[i]->conv_enabled || cs[i]->comm) {
+        cs[i]->steps_done != c0->steps_done || cs[i]->cur != c0->cur || cs[i]->conv_enabled || cs[i]->comm) {
       c0->err = "lbm_group_step: slabs must share device, row layout (nx, ny, x_align) and step count, "
                 "without convergence control or RCCL";
       return LBM_ERR_ARG;
@@ -1353,18 +1519,19 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   HIPCK(c0, hipMemcpy(dconvs, hc.data(), sizeof(ConvState*) * n, hipMemcpyHostToDevice));
   RCK(ensure_hist(c0, std::max(nsteps, 1)));
   if (!c0->halo_primed) {
-    RCK(loopback_exchange(cs, n, c0->steps_done & 1, true, st));
+    RCK(loopback_exchange(cs, n, c0->cur, true, st));
     for (int i = 0; i < n; ++i) cs[i]->halo_primed = true;
   }
   int h = c0->steps_done;
   for (int s = 0; s < nsteps; ++s, ++h) {
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      RCK(run_range(c, c->edge, h, st));
-      RCK(run_range(c, c->mid, h, st));
+      RCK(run_range(c, c->edge, h, c0->cur, st));
+      RCK(run_range(c, c->mid, h, c0->cur, st));
       HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
     }
-    RCK(loopback_exchange(cs, n, (h + 1) & 1, false, st));
+    RCK(loopback_exchange(cs, n, c0->cur ^ 1, false, st));
+    for (int i = 0; i < n; ++i) cs[i]->cur ^= 1;
     hipLaunchKernelGGL(k_sum_locals, dim3(1), dim3(1), 0, st, dconvs, n);
     for (int i = 0; i < n; ++i)
       HIPCK(c0, launch_finish_global(cs[i]->conv, (i == 0 && residual_hist) ? c0->hist + s : nullptr, st));
@@ -1373,6 +1540,7 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   for (int i = 0; i < n; ++i) {
     cs[i]->steps_done += nsteps;
     cs[i]->macros_stale = true;
+    cs[i]->macros_stored = false;
     cs[i]->last_slab = true;
   }
   if (residual_hist && nsteps > 0)

@@ -33,7 +33,7 @@ LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_BC_PRESSURE = 0, 1, 2
 LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
 # lbm_tune knobs (include/lbm.h lbm_tune_knob)
 (TUNE_ROW_AXIS, TUNE_CELLS_PER_LANE, TUNE_EXACT_DIV, TUNE_FUSED_RESIDUAL, TUNE_BUFFER_ALLOC,
- TUNE_SYNC_TIMEOUT_S, TUNE_BUFFER_GAP_KB) = range(7)
+ TUNE_SYNC_TIMEOUT_S, TUNE_STEPS_PER_LAUNCH) = range(7)
 
 # reference per-case constants
 LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55
@@ -85,7 +85,7 @@ LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_tune", "lbm_get_nonfinite", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
-    "lbm_get_layout",
+    "lbm_get_layout", "lbm_buffer_placement",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream",
 ]
 HOST_SYMBOLS = [
@@ -169,6 +169,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
             "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
             "lbm_get_layout": (C.c_int, [P, ip, ip, ip, i64p]),
+            "lbm_buffer_placement": (C.c_int, [P, f64p, C.c_int, ip, ip]),
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_comm_info": (C.c_int, [P, ip, ip]),
@@ -478,6 +479,13 @@ class Lattice:
         self._ck(lbm_lib().lbm_get_numerics(self.h, C.byref(fd), C.byref(n)), "lbm_get_numerics")
         return {"fast_div": bool(fd.value), "retried_chunks": n.value}
 
+    def placement(self):
+        """Population-buffer placement (lbm_buffer_placement): candidates' write rates (GB/s) and
+        the two kept; an empty list when the first two allocations were taken unprobed."""
+        gbs, n, ch = (C.c_double * 8)(), C.c_int(), (C.c_int * 2)()
+        self._ck(lbm_lib().lbm_buffer_placement(self.h, gbs, 8, C.byref(n), ch), "lbm_buffer_placement")
+        return {"candidate_write_gbs": [round(gbs[i], 1) for i in range(min(n.value, 8))], "chosen": [ch[0], ch[1]]}
+
     def profile(self, enabled: bool = True):
         self._ck(lbm_lib().lbm_profile(self.h, 1 if enabled else 0), "lbm_profile")
 
@@ -486,7 +494,7 @@ class Lattice:
         self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
         out = {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
         for kind, name in ((0, "step_kernel"), (1, "step_kernel_src0"), (2, "step_kernel_src1"), (3, "edge"),
-                           (4, "interior"), (5, "halo"), (6, "halo_exposed")):
+                           (4, "interior"), (5, "halo"), (6, "halo_exposed"), (7, "two_step")):
             m, k = C.c_double(), C.c_int64()
             self._ck(lbm_lib().lbm_kernel_times(self.h, kind, C.byref(m), C.byref(k)), "lbm_kernel_times")
             out[name + "_ms"], out[name + "_launches"] = m.value, k.value
