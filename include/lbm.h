@@ -147,11 +147,7 @@ typedef enum {
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
                                    asynchronous RCCL error always aborts promptly. */
-  LBM_TUNE_STEPS_PER_LAUNCH = 6, /* 0 (default) and 1: one time step per launch; 2: two per launch
-                                   (k_step2, LDS temporal blocking) wherever allowed (single
-                                   domain, no convergence control, rows a multiple of 64 slots);
-                                   slower at 512^3, kept as the measured LDS-staged alternative */
-  LBM_TUNE_COUNT = 7
+  LBM_TUNE_COUNT = 6
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

@@ -33,7 +33,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -46,8 +46,7 @@ enum : int {
   kKindMid = 4,        // slab step: the interior launch
   kKindHalo = 5,       // slab step: halo pack -> send/recv -> unpack on the communication stream
   kKindExposed = 6,    // slab step: halo end after interior end (clipped at 0): the exchange not hidden
-  kKindTwoStep = 7,    // k_step2 launches (two time steps each)
-  kKinds = 8
+  kKinds = 7
 };
 
 struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) with their work lists
@@ -58,7 +57,6 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int* cells = nullptr;   // NEE-adjacent fluid cells
   int nslow = 0;
   float4* prev = nullptr; // their (rho, u) of the previous step
-  float4* prev_alt = nullptr;  // k_step2's output copy (swapped with prev after each two-step launch)
   uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
   float4* nee_bc = nullptr;   // their first kNeeSlots NEE neighbours' boundary data (static)
   double* part = nullptr; // main partials, then fix-up partials
@@ -119,11 +117,6 @@ struct lbm_ctx {
   // lazy macros (k_moments): the step kernels store none; lbm_get_macros recomputes them
   // from the last step's source buffer when macros_stale
   bool macros_stale = false;
-  bool macros_stored = false;  // the last launch stored (rho, u) itself (k_step2 on a call's last launch)
-  // two steps per launch (k_step2, single domain): per-cell NEE-list index, step t+2 partials
-  int* nee_idx = nullptr;
-  double* part2 = nullptr;
-  int step2_nblk = 0;
   bool last_slab = false;  // the last steps ran the slab ranges (edge + mid), not whole
   // rccl
   ncclComm_t comm = nullptr;
@@ -451,7 +444,6 @@ void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
-  if (r.prev_alt) (void)hipFree(r.prev_alt);
   if (r.nee_mask) (void)hipFree(r.nee_mask);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
@@ -483,7 +475,6 @@ int reset_state(lbm_ctx* c) {
   }
   c->steps_done = 0;
   c->cur = 0;
-  c->macros_stored = false;
   c->halo_primed = false;
   c->macros_stale = false;
   return LBM_OK;
@@ -572,7 +563,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 2};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -835,8 +826,6 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->bc_in) (void)hipFree(c->bc_in);
   if (c->bc_out) (void)hipFree(c->bc_out);
   if (c->partial_all) (void)hipFree(c->partial_all);
-  if (c->nee_idx) (void)hipFree(c->nee_idx);
-  if (c->part2) (void)hipFree(c->part2);
   if (c->red_part) (void)hipFree(c->red_part);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
@@ -1017,74 +1006,15 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
   return LBM_OK;
 }
 
-// k_step2 geometry: planes per z run (units = tiles x runs: enough for a few rounds of the
-// 256 CUs, runs long enough that the two pipeline-fill planes per run stay a few percent)
-int step2_zlen(const lbm_ctx* c) {
-  const int64_t tiles = (int64_t)((c->L.pitch + 63) / 64) * ((c->L.plane / c->L.pitch + 5) / 6);
-  const int64_t z = (int64_t)c->L.nz * tiles / 2048;
-  return (int)std::max<int64_t>(16, std::min<int64_t>(64, z));
-}
-
-// two steps per launch (LBM_TUNE_STEPS_PER_LAUNCH = 2): single domain, no convergence control
-// (the stop must be known after every step), rows a multiple of 64 slots.  Opt-in: at 512^3 k_step2 measured 5.07 ms per step
-// against k_step's 3.7 ("Two steps per launch"), so the default is one.
-bool use_step2(const lbm_ctx* c) {
-  return g_tune[LBM_TUNE_STEPS_PER_LAUNCH] == 2 && !c->conv_enabled && !c->comm && c->L.pitch % 64 == 0;
-}
-
-int ensure_step2(lbm_ctx* c) {
-  if (c->nee_idx) return LBM_OK;
-  const int nblk = step2_blocks(c->L.pitch, (int)(c->L.plane / c->L.pitch), c->L.nz, step2_zlen(c));
-  HIPCK(c, hipMalloc(&c->part2, sizeof(double) * 2 * nblk));
-  c->step2_nblk = nblk;
-  HIPCK(c, hipMalloc(&c->nee_idx, sizeof(int) * c->L.ncell));
-  HIPCK(c, hipMemsetAsync(c->nee_idx, 0xFF, sizeof(int) * c->L.ncell, c->s_comp));
-  HIPCK(c, launch_scatter_idx(c->whole.cells, c->whole.nslow, c->nee_idx, c->s_comp));
-  if (c->whole.nslow) HIPCK(c, hipMalloc(&c->whole.prev_alt, sizeof(float4) * c->whole.nslow));
-  return LBM_OK;
-}
-
-// steps h and h + 1 in one k_step2 launch, buf[cur] -> buf[cur ^ 1]; store: the call's last
-// launch, which stores (rho, u) itself (no source buffer of step h + 1 to recompute them from)
-int run_step2(lbm_ctx* c, int h, bool store, float* hist) {
-  MainArgs a{};
-  fill_main_args(c, a, c->cur);
-  a.partial = c->part2;
-  a.nee_active = h == 0 ? 0 : 1;
-  a.prev = c->whole.prev; a.nee_mask = c->whole.nee_mask; a.nee_bc = c->whole.nee_bc;
-  const int nblk = c->step2_nblk;
-  c->launches++;
-  RCK(timed(c, c->s_comp, kKindStep, kKindSrc0 + c->cur, kKindTwoStep, [&] {
-    HIPCK(c, launch_step2(a, c->whole.prev_alt, c->nee_idx, c->part2 + nblk, (int)(c->L.plane / c->L.pitch), c->L.nz,
-                          step2_zlen(c), c->L.ncell, store ? 1 : 0, c->s_comp));
-    return LBM_OK;
-  }));
-  c->cur ^= 1;
-  std::swap(c->whole.prev, c->whole.prev_alt);
-  HIPCK(c, launch_reduce(c->part2, nblk, c->scratch, c->conv, hist, 1, c->s_comp));
-  HIPCK(c, launch_reduce(c->part2 + nblk, nblk, c->scratch, c->conv, hist ? hist + 1 : nullptr, 1, c->s_comp));
-  return LBM_OK;
-}
-
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
   int h = c->steps_done;
-  int s0 = 0;
-  c->macros_stored = false;
-  if (use_step2(c) && nsteps >= 2) {
-    RCK(ensure_step2(c));
-    for (; s0 + 2 <= nsteps; s0 += 2, h += 2) RCK(run_step2(c, h, s0 + 2 == nsteps, want_hist ? c->hist + s0 : nullptr));
-    if (s0 == nsteps) {
-      c->macros_stored = true;
-      return LBM_OK;
-    }
-  }
   if (c->fuse_red && !c->conv_enabled) {
     // one launch per step: step s's k_step also finishes step s-1's residual; the last
     // step's own reduction follows the loop
     const double* prev = nullptr;
-    for (int s = s0; s < nsteps; ++s, ++h) {
+    for (int s = 0; s < nsteps; ++s, ++h) {
       double* part = c->red_part + (size_t)(s & 1) * c->red_n;
-      const FusedRed fr{part, prev, (want_hist && s > s0) ? c->hist + s - 1 : nullptr};
+      const FusedRed fr{part, prev, (want_hist && s > 0) ? c->hist + s - 1 : nullptr};
       RCK(run_range(c, c->whole, h, c->cur, c->s_comp, &fr));
       c->cur ^= 1;
       prev = part;
@@ -1093,7 +1023,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
                            c->s_comp));
     return LBM_OK;
   }
-  for (int s = s0; s < nsteps; ++s, ++h) {
+  for (int s = 0; s < nsteps; ++s, ++h) {
     RCK(run_range(c, c->whole, h, c->cur, c->s_comp));
     c->cur ^= 1;
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
@@ -1178,7 +1108,7 @@ int refresh_macros(lbm_ctx* c) {
   HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
   c->steps_done = h.k;
   c->macros_stale = false;
-  if (h.k == 0 || c->macros_stored) return LBM_OK;  // no step ran (initial arrays), or stored by k_step2
+  if (h.k == 0) return LBM_OK;  // no step ran: the initial arrays
   const Layout& L = c->L;
   const float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
   HIPCK(c, launch_moments(src, c->type, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
@@ -1540,7 +1470,6 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   for (int i = 0; i < n; ++i) {
     cs[i]->steps_done += nsteps;
     cs[i]->macros_stale = true;
-    cs[i]->macros_stored = false;
     cs[i]->last_slab = true;
   }
   if (residual_hist && nsteps > 0)

@@ -1044,323 +1044,6 @@ __global__ void k_digest(const uint8_t* __restrict__ type, const float* __restri
   if (threadIdx.x == 0) atomicAdd(out + zl, part[0] + part[1] + part[2] + part[3]);
 }
 
-// ---- two steps per launch (temporal blocking through LDS) -----------------------------------
-//
-// k_step2 advances a single-domain lattice by two time steps in one pass over HBM: every
-// population is loaded once (time t) and stored once (time t+2).  Work unit = a tile of
-// kT2W x kT2H storage cells (64 slots of a row x 6 rows; c-space, so the row shift and the
-// row axis need no special case) over a run of z planes.  The workgroup's 9 waves own the
-// tile's columns plus a one-cell ring (66 x 8) and march up the z run:
-//
-//   step 1, plane p   (all columns of the ring; wave w < 8 = ring row w, wave 8 = the 16
-//                      x-halo cells): the one-step update of process_cell1 -- pulls from the
-//                      source buffer (producer-side wall slots, NEE substitution from the
-//                      previous step's kept (rho, u)), BGK -- into an LDS ring of three
-//                      planes, all 19 populations.  Cells that are pulled raw (NEE cells,
-//                      passive cells a fluid cell pulls) copy their constant slots instead.
-//   step 2, plane p-1 (the tile's own columns, waves 1..6): pulls from the LDS ring --
-//                      bounce-back on the consumer side (the wall slot a cell pulls is its own
-//                      outgoing f_opp of step 1, the value its producer-side store would have
-//                      put there), NEE from its own step-1 slot and step-1 (rho, u), the latter
-//                      carried in registers from the previous iteration (same thread, same
-//                      column) -- BGK, stores of t+2 into the destination buffer with the
-//                      producer-side wall slots, as k_step does.
-//
-// One barrier per plane: the ring has four plane slots, so the step 1 of the next plane
-// writes a slot no wave still reads.  Each wave issues the pulls of the plane two ahead before
-// the arithmetic of the current one (two register sets).  Row waves address a 64-slot run of a
-// row as a wave-uniform base plus the lane (tiles are 64-aligned and the pitch a multiple of
-// 64, so a run never straddles a 256-cell chunk; an x-shifted pull fixes its one straddling
-// lane with a scalar load, as k_step does).  Results are bit-identical to two k_step launches:
-// the same expression trees in the same order; only the place a value is read from changes.
-// |u| partials: step t+1 over the tile's own cells (partial), step t+2 (partial2).
-constexpr int kT2W = 64, kT2H = 6;                 // step-2 tile: slots x rows
-constexpr int kT1W = kT2W + 2, kT1H = kT2H + 2;    // step-1 ring
-constexpr int kT1N = kT1W * kT1H;                  // 528 LDS cells per plane slot
-constexpr int kRing = 4;                           // plane slots
-constexpr int kStep2Threads = (kT1H + 1) * 64;     // 8 row waves + 1 x-halo wave
-constexpr size_t kStep2Lds = sizeof(float) * kRing * kQ * kT1N;
-
-struct Step2Args {
-  MainArgs m;            // src, dst, type, links, macros, tau, NEE lists (prev, nee_mask, nee_bc) ...
-  const int* nee_idx;    // per cell: index into the NEE-adjacent lists (-1: not NEE-adjacent)
-  double* partial2;      // step t+2 |u| partial per block (m.partial: step t+1)
-  float4* prev_out;      // (rho, u) of step t+2 per NEE-adjacent cell (m.prev: of step t, read only --
-                         // a tile's ring reads cells other tiles own and update in the same launch)
-  int n1;                // storage rows per plane
-  int ntx, nty;          // tiles per row / per plane
-  int zlen, nzr;         // planes per z run (a multiple of 4), z runs
-  int nz;                // local planes
-  int64_t ncell;
-  int store_macros;      // store (rho, u) of step t+2 for every fluid cell (the call's last launch)
-};
-
-template <bool SW, int... Qs>
-__device__ __forceinline__ void own1_all(float* f, const float* __restrict__ src, int64_t c,
-                                         std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = src[aidx(c, Qs)]), ...);
-}
-
-// pull of population Q for lane `lane` of a row run starting at cell R (wave-uniform, a
-// multiple of 64): the 64 cells R - e_Q .. R + 63 - e_Q
-template <int Q, bool SW>
-__device__ __forceinline__ float pull_run(const float* __restrict__ src, int64_t R, unsigned lane, int pitch,
-                                          int64_t plane) {
-  const int64_t S = R - row_off<Q, SW>(pitch, plane);  // the run for e_x = 0: one chunk slice
-  const float* base = src + ((S >> 8) * kQ + Q) * kChunk + (S & (kChunk - 1));
-  if constexpr (SDir<Q, SW>::x == 0) {
-    return base[lane];
-  } else if constexpr (SDir<Q, SW>::x == 1) {  // cells S - 1 .. S + 62: lane 0 may sit in the chunk before
-    const float v = base[lane - 1];
-    const float e = src[aidx(S - 1, Q)];
-    return lane == 0 ? e : v;
-  } else {                                     // cells S + 1 .. S + 64: lane 63 may sit in the next chunk
-    const float v = base[lane + 1];
-    const float e = src[aidx(S + 64, Q)];
-    return lane == 63 ? e : v;
-  }
-}
-
-template <bool SW, int... Qs>
-__device__ __forceinline__ void pull_run_all(float* f, const float* __restrict__ src, int64_t R, unsigned lane,
-                                             int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = pull_run<Qs, SW>(src, R, lane, pitch, plane)), ...);
-}
-
-// step-2 pull of population Q for the cell at LDS index li from ring slots (plane p - 1, p, p + 1)
-template <int Q, bool SW, int SM, int S0, int SP>
-__device__ __forceinline__ float lds_pull(const float* lds, int li, uint32_t wl) {
-  if constexpr (Q == 0) {
-    return lds[(S0 * kQ + 0) * kT1N + li];
-  } else {
-    if (wl & (1u << Q)) return lds[(S0 * kQ + Dir<Q>::opp) * kT1N + li];  // wall: own outgoing opp
-    constexpr int dz = SDir<Q, SW>::z;
-    constexpr int slot = dz == 1 ? SM : dz == -1 ? SP : S0;               // pull from plane p - dz
-    return lds[(slot * kQ + Q) * kT1N + li - (SDir<Q, SW>::y * kT1W + SDir<Q, SW>::x)];
-  }
-}
-
-template <bool SW, int SM, int S0, int SP, int... Qs>
-__device__ __forceinline__ void lds_pull_all(float* f, const float* lds, int li, uint32_t wl,
-                                             std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = lds_pull<Qs, SW, SM, S0, SP>(lds, li, wl)), ...);
-}
-
-template <int S, int... Qs>
-__device__ __forceinline__ void lds_put_all(float* lds, int li, const float* f, std::integer_sequence<int, Qs...>) {
-  ((lds[(S * kQ + Qs) * kT1N + li] = f[Qs]), ...);
-}
-
-// row-run store of the 19 populations of lane `lane` (cells R .. R + 63, one chunk slice)
-template <int... Qs>
-__device__ __forceinline__ void store_run_all(float* __restrict__ dst, int64_t R, unsigned lane, const float* f,
-                                              std::integer_sequence<int, Qs...>) {
-  float* base = dst + (R >> 8) * kQ * kChunk + (R & (kChunk - 1));
-  ((base[Qs * kChunk + lane] = f[Qs]), ...);
-}
-
-__device__ __forceinline__ void moments1(const float* f, float& rho, float& ux, float& uy, float& uz) {
-  float r = 0.f;
-#pragma unroll
-  for (int q = 0; q < kQ; ++q) r = r + f[q];
-  ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / r;
-  uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / r;
-  uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / r;
-  rho = r;
-}
-
-// producer-side bounce-back slots of a wall-adjacent cell (fix_store_all without the 19 own stores)
-template <bool SW, int... Qs>
-__device__ __forceinline__ void bb_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m, int pitch,
-                                             int64_t plane, std::integer_sequence<int, Qs...>) {
-  (bb_store_one<Qs, SW>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
-}
-
-// per-thread state of the z march
-struct March {
-  float pre[2][kQ];      // pulls of the next two step-1 planes
-  uint8_t tpre[2];
-  uint32_t lpre[2];
-  uint8_t t_prev;        // type / links / step-1 macros of this column's cell one plane below
-  uint32_t l_prev;
-  float rho_p, ux_p, uy_p, uz_p;
-  double acc1, acc2;
-};
-
-template <bool SW>
-struct Tile2 {
-  const Step2Args& A;
-  int za, zb;            // step-2 planes [za, zb) (local z)
-  int y0, x0, r, col, li;
-  unsigned lane;
-  bool rowwave, act1, act2, rowin;
-  int64_t off;           // storage offset of this thread's step-1 cell within a plane
-  int64_t rbase;         // row waves: offset of the run's first cell (wave-uniform)
-
-  // type, wall links and pulls of this thread's step-1 cell in storage plane zs
-  __device__ __forceinline__ void issue(int zs, float* f, uint8_t& t, uint32_t& l) const {
-    const MainArgs& a = A.m;
-    const bool ghost = zs == 0 || zs == A.nz + 1;
-    if (rowwave) {
-      t = kPassive;
-      l = 0;
-      if (!rowin) return;  // ring row outside the plane's rows: nothing there (wave-uniform)
-      const int64_t R = (int64_t)zs * a.plane + rbase;  // the run's first cell
-      t = a.type[R + lane];
-      l = a.links[R + lane];
-      if (!ghost) pull_run_all<SW>(f, a.src, R, lane, a.pitch, a.plane, AllQ{});
-      return;
-    }
-    int64_t c = (int64_t)zs * a.plane + off;
-    const bool in = act1 && c >= 0 && c < A.ncell;
-    if (!in) c = 0;
-    t = in ? a.type[c] : (uint8_t)kPassive;
-    l = a.links[c];
-    if (!ghost) pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
-  }
-};
-
-template <bool SW, int S1, int SM, int S0, int SP, int PB>
-__device__ __forceinline__ void step2_iter(const Tile2<SW>& T, March& M, float* lds, int zs) {
-  const Step2Args& A = T.A;
-  const MainArgs& a = A.m;
-  float f[kQ];
-#pragma unroll
-  for (int q = 0; q < kQ; ++q) f[q] = M.pre[PB][q];
-  const uint8_t t = M.tpre[PB];
-  const uint32_t lk = M.lpre[PB];
-  if (zs + 2 <= T.zb + 1) T.issue(zs + 2, M.pre[PB], M.tpre[PB], M.lpre[PB]);  // two planes ahead
-  // ---- step 1 at storage plane zs; ghost planes (storage 0 and nz + 1) are never updated by a
-  // single-domain step, so their cells are pulled raw, as constants
-  const bool ghost = zs == 0 || zs == A.nz + 1;
-  const int cls = ghost ? kNee : (t & kClassMask);
-  const int64_t c = (int64_t)zs * a.plane + T.off;
-  float r1 = 0.f, x1 = 0.f, y1 = 0.f, z1 = 0.f;
-  if (cls == kFluid) {
-    if ((t & kNeedsMac) && a.nee_active) {  // NEE substitution (nee_cell): reload with the list data
-      const int i = A.nee_idx[c];
-      const float4 pv = a.prev[i];
-      const Macro mp{pv.x, pv.y, pv.z, pv.w};
-      float4 bc[kNeeSlots];
-#pragma unroll
-      for (int j = 0; j < kNeeSlots; ++j) bc[j] = a.nee_bc[(int64_t)i * kNeeSlots + j];
-      nee_pull_all<SW>(f, a, c, mp, a.nee_mask[i], bc, AllQ{});
-    }
-    moments1(f, r1, x1, y1, z1);
-    relax1(f, a, r1, x1, y1, z1);
-    lds_put_all<S1>(lds, T.li, f, AllQ{});
-    if (T.act2 && zs >= T.za + 1 && zs <= T.zb) M.acc1 += (double)sqrtf(x1 * x1 + y1 * y1 + z1 * z1);
-  } else if (T.act1 && (cls == kNee || (cls == kPassive && (t & kPulled)) || (ghost && (t & kClassMask) == kFluid))) {
-    own1_all<SW>(f, a.src, c, AllQ{});  // pulled raw: constant slots
-    lds_put_all<S1>(lds, T.li, f, AllQ{});
-  }
-  __syncthreads();
-  // ---- step 2 at storage plane p = zs - 1
-  const int p = zs - 1;
-  if (T.act2 && p >= T.za + 1 && p <= T.zb && (M.t_prev & kClassMask) == kFluid) {
-    const uint8_t tp = M.t_prev;
-    const int64_t cp = (int64_t)p * a.plane + T.off;
-    const uint32_t wl = (tp & kWallAdj) ? M.l_prev : 0u;
-    float g[kQ];
-    lds_pull_all<SW, SM, S0, SP>(g, lds, T.li, wl, AllQ{});
-    int i = -1;
-    if (tp & kNeedsMac) {  // NEE values from the cell's own step-1 slots and step-1 (rho, u)
-      i = A.nee_idx[cp];
-      const uint2 mk = a.nee_mask[i];
-      const Macro mp{M.rho_p, M.ux_p, M.uy_p, M.uz_p};
-      uint32_t rest = mk.x;
-      for (int j = 0; rest; ++j) {
-        const int q = __builtin_ctz(rest);
-        rest &= rest - 1u;
-        float4 b;
-        if (j < kNeeSlots) {
-          b = a.nee_bc[(int64_t)i * kNeeSlots + j];
-        } else {
-          const int64_t nb = cp - cell_off_rt<SW>(q, a.pitch, a.plane);
-          b = make_float4(a.rho[nb], a.ux[nb], a.uy[nb], a.uz[nb]);
-        }
-        const NeeSlot sl = nee_slot(lds[(S0 * kQ + q) * kT1N + T.li], b);
-        g[q] = nee_value_rt(q, sl, mp, (mk.y >> q) & 1u, a.omc);
-      }
-    }
-    float r2, x2, y2, z2;
-    moments1(g, r2, x2, y2, z2);
-    relax1(g, a, r2, x2, y2, z2);
-    store_run_all(a.dst, (int64_t)p * a.plane + T.rbase, T.lane, g, AllQ{});  // step 2: row waves only
-    if (wl) bb_store_all<SW>(g, a.dst, cp, wl, a.pitch, a.plane, AllQ{});
-    if (i >= 0) A.prev_out[i] = make_float4(r2, x2, y2, z2);
-    if (A.store_macros) {
-      a.rho[cp] = r2; a.ux[cp] = x2; a.uy[cp] = y2; a.uz[cp] = z2;
-    }
-    M.acc2 += (double)sqrtf(x2 * x2 + y2 * y2 + z2 * z2);
-  }
-  M.rho_p = r1; M.ux_p = x1; M.uy_p = y1; M.uz_p = z1;
-  M.t_prev = t;
-  M.l_prev = lk;
-}
-
-template <bool SW>
-__global__ __launch_bounds__(kStep2Threads) void k_step2(const Step2Args A) {
-  extern __shared__ float lds[];
-  __shared__ double red[kStep2Threads / 64];
-  const MainArgs& a = A.m;
-  const unsigned lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // XCD-aware unit order: blocks b, b + 8, ... share an XCD; each XCD takes one contiguous run
-  // of units, neighbouring y tiles first, so the ring rows two tiles share meet in its L2
-  const int nunits = A.ntx * A.nty * A.nzr;
-  const int per_xcd = (nunits + 7) / 8;
-  const int unit = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  March M{};
-  if (unit < nunits) {
-    Tile2<SW> T{A};
-    const int ty = unit % A.nty, rest = unit / A.nty;
-    const int tx = rest % A.ntx, zr = rest / A.ntx;
-    T.x0 = tx * kT2W;
-    T.y0 = ty * kT2H;
-    T.za = zr * A.zlen;
-    T.zb = min(A.nz, T.za + A.zlen);
-    T.lane = lane;
-    T.rowwave = wave < kT1H;
-    T.act1 = T.rowwave || lane < 2 * kT1H;
-    T.r = 0;
-    T.col = 0;
-    if (T.rowwave) {
-      T.r = wave;
-      T.col = (int)lane;
-    } else if (T.act1) {
-      T.r = (int)lane >> 1;
-      T.col = (lane & 1) ? kT2W : -1;
-    }
-    const int row = T.y0 - 1 + T.r;
-    T.rowin = row >= 0 && row < A.n1;  // wave-uniform for the row waves
-    T.li = T.r * kT1W + T.col + 1;
-    T.off = (int64_t)row * a.pitch + (T.x0 + T.col);
-    T.rbase = (int64_t)row * a.pitch + T.x0;
-    T.act2 = wave >= 1 && wave <= kT2H && row < A.n1 && (T.x0 + T.col) < a.pitch;
-    // prologue: the pulls of the first two step-1 planes (storage za, za + 1)
-    T.issue(T.za, M.pre[0], M.tpre[0], M.lpre[0]);
-    T.issue(T.za + 1, M.pre[1], M.tpre[1], M.lpre[1]);
-    // storage planes za .. zb + 1, four per trip (ring slot = k % 4, register set = k % 2)
-    for (int zs = T.za; zs <= T.zb + 1; zs += 4) {
-      step2_iter<SW, 0, 2, 3, 0, 0>(T, M, lds, zs);
-      if (zs + 1 > T.zb + 1) break;
-      step2_iter<SW, 1, 3, 0, 1, 1>(T, M, lds, zs + 1);
-      if (zs + 2 > T.zb + 1) break;
-      step2_iter<SW, 2, 0, 1, 2, 0>(T, M, lds, zs + 2);
-      if (zs + 3 > T.zb + 1) break;
-      step2_iter<SW, 3, 1, 2, 3, 1>(T, M, lds, zs + 3);
-    }
-  }
-  double s1 = block_sum(M.acc1, red);
-  __syncthreads();
-  const double s2 = block_sum(M.acc2, red);
-  if (threadIdx.x == 0) {
-    a.partial[blockIdx.x] = s1;
-    A.partial2[blockIdx.x] = s2;
-  }
-}
-
 int grid_for(int64_t n, int block) {
   int64_t g = (n + block - 1) / block;
   if (g > 65536) g = 65536;
@@ -1539,53 +1222,6 @@ hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux,
   const int per_plane = std::max(1, std::min(256, (int)(plane / 4096)));
   hipLaunchKernelGGL(k_digest, dim3(per_plane, nz), dim3(256), 0, s, type, rho, ux, uy, uz, nx, ny, pitch, xshift,
                      plane, z_offset, swap, out);
-  return hipGetLastError();
-}
-
-__global__ void k_scatter_idx(const int* __restrict__ cells, int n, int* __restrict__ idx) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) idx[cells[i]] = i;
-}
-
-hipError_t launch_scatter_idx(const int* cells, int n, int* idx, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter_idx, dim3((n + 255) / 256), dim3(256), 0, s, cells, n, idx);
-  return hipGetLastError();
-}
-
-int step2_blocks(int pitch, int n1, int nz, int zlen) {
-  const int ntx = (pitch + kT2W - 1) / kT2W, nty = (n1 + kT2H - 1) / kT2H, nzr = (nz + zlen - 1) / zlen;
-  return (ntx * nty * nzr + 7) / 8 * 8;
-}
-
-hipError_t launch_step2(const MainArgs& m, float4* prev_out, const int* nee_idx, double* partial2, int n1, int nz,
-                        int zlen, int64_t ncell, int store_macros, hipStream_t s) {
-  // row waves address 64-slot runs as a wave-uniform base + lane: tiles must not straddle rows
-  if (m.pitch % kT2W != 0) return hipErrorInvalidValue;
-  Step2Args A{};
-  A.m = m;
-  A.prev_out = prev_out;
-  A.nee_idx = nee_idx;
-  A.partial2 = partial2;
-  A.n1 = n1;
-  A.ntx = (m.pitch + kT2W - 1) / kT2W;
-  A.nty = (n1 + kT2H - 1) / kT2H;
-  A.zlen = zlen;
-  A.nzr = (nz + zlen - 1) / zlen;
-  A.nz = nz;
-  A.ncell = ncell;
-  A.store_macros = store_macros;
-  const int blocks = step2_blocks(m.pitch, n1, nz, zlen);
-  typedef void (*Kern)(const Step2Args);
-  static bool attr_set[2] = {false, false};
-  const Kern k = m.swap ? k_step2<true> : k_step2<false>;
-  if (!attr_set[m.swap ? 1 : 0]) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)kStep2Lds);
-    if (e != hipSuccess) return e;
-    attr_set[m.swap ? 1 : 0] = true;
-  }
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(kStep2Threads), kStep2Lds, s, A);
   return hipGetLastError();
 }
 

@@ -144,13 +144,6 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
                          int finish, hipStream_t s,
                          double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
-// two steps per launch (single domain, LDS temporal blocking): partials m.partial (step t+1)
-// and partial2 (step t+2), step2_blocks() of each; nee_idx per cell -> NEE-adjacent list index
-int step2_blocks(int pitch, int n1, int nz, int zlen);
-// idx[cells[i]] = i (the per-cell index of a cell list; idx pre-filled with -1)
-hipError_t launch_scatter_idx(const int* cells, int n, int* idx, hipStream_t s);
-hipError_t launch_step2(const MainArgs& m, float4* prev_out, const int* nee_idx, double* partial2, int n1, int nz,
-                        int zlen, int64_t ncell, int store_macros, hipStream_t s);
 // lazy macros: (rho, u) of the fluid cells in [lo, hi) from the last step's source buffer
 // (NEE-adjacent cells excepted), then those cells' kept (rho, u)
 hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,

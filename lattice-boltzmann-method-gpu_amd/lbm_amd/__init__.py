@@ -33,7 +33,7 @@ LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_BC_PRESSURE = 0, 1, 2
 LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
 # lbm_tune knobs (include/lbm.h lbm_tune_knob)
 (TUNE_ROW_AXIS, TUNE_CELLS_PER_LANE, TUNE_EXACT_DIV, TUNE_FUSED_RESIDUAL, TUNE_BUFFER_ALLOC,
- TUNE_SYNC_TIMEOUT_S, TUNE_STEPS_PER_LAUNCH) = range(7)
+ TUNE_SYNC_TIMEOUT_S) = range(6)
 
 # reference per-case constants
 LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55
@@ -494,7 +494,7 @@ class Lattice:
         self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
         out = {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
         for kind, name in ((0, "step_kernel"), (1, "step_kernel_src0"), (2, "step_kernel_src1"), (3, "edge"),
-                           (4, "interior"), (5, "halo"), (6, "halo_exposed"), (7, "two_step")):
+                           (4, "interior"), (5, "halo"), (6, "halo_exposed")):
             m, k = C.c_double(), C.c_int64()
             self._ck(lbm_lib().lbm_kernel_times(self.h, kind, C.byref(m), C.byref(k)), "lbm_kernel_times")
             out[name + "_ms"], out[name + "_launches"] = m.value, k.value
