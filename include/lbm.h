@@ -81,6 +81,11 @@ typedef struct {
    * lbm_create. */
   const float* u_normal_table;
 } lbm_bc_code;
+/* Boundary data are static for a context's lifetime: the (rho_bc, u_bc) of every NEE cell --
+ * lid speed, inlet/outlet tables, bc_codes -- is fixed by lbm_create and the lbm_init_* call,
+ * and each NEE-adjacent fluid cell's work list gathers its boundary neighbours' data once, when
+ * the lists are built.  No entry point changes them later; one that did would have to rebuild
+ * (re-gather) those lists as well. */
 
 /* Equilibrium expression used to initialise f (the two forms of the reference). */
 typedef enum {

@@ -125,6 +125,65 @@ void lbmh_geo_mask(int nx, int ny, int nz, const int32_t* raw, int8_t* geo) {
   for (int64_t c = 0; c < b.size(); ++c) geo[c] = (int8_t)g[c];
 }
 
+long lbmh_read_geo_txt_zxy(const char* path, int nx, int ny, int nz, int32_t* raw) {
+  FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  const Box b{nx, ny, nz};
+  long i = 0;
+  int v;
+  for (int z = 0; z < nz; ++z)
+    for (int x = 0; x < nx; ++x)
+      for (int y = 0; y < ny; ++y) {
+        if (std::fscanf(f, "%d ", &v) != 1) {
+          std::fclose(f);
+          return i;
+        }
+        raw[b(x, y, z)] = v;
+        ++i;
+      }
+  std::fclose(f);
+  return i;
+}
+
+void lbmh_geo_ends(int nx, int ny, int nz, const int32_t* raw, int n_ends, const lbmh_end* ends, int8_t* geo) {
+  const Box b{nx, ny, nz};
+  std::vector<int> g(raw, raw + b.size());
+  // fluid: three increments of the 6-neighbour minimum of the (unchanged) raw mask
+  for (int z = 1; z < nz - 1; ++z)
+    for (int y = 1; y < ny - 1; ++y)
+      for (int x = 1; x < nx - 1; ++x) g[b(x, y, z)] += 3 * min6(raw, b, x, y, z);
+  // ends: in-plane 4-neighbour minimum, `passes` times; increments commute, so ends that
+  // share cells (an x plane crossing a z plane) add up as the reference's sequence does
+  for (int e = 0; e < n_ends; ++e) {
+    const lbmh_end& E = ends[e];
+    for (int s1 = E.lo1; s1 < E.hi1; ++s1)
+      for (int s0 = E.lo0; s0 < E.hi0; ++s0) {
+        int x, y, z, m;
+        if (E.axis == 0) {
+          x = E.plane; y = s0; z = s1;
+          m = std::min({raw[b(x, y - 1, z)], raw[b(x, y + 1, z)], raw[b(x, y, z - 1)], raw[b(x, y, z + 1)]});
+        } else {
+          x = s0; y = s1; z = E.plane;
+          m = std::min({raw[b(x, y - 1, z)], raw[b(x, y + 1, z)], raw[b(x - 1, y, z)], raw[b(x + 1, y, z)]});
+        }
+        g[b(x, y, z)] += E.passes * m;
+      }
+  }
+  mark_ghosts(b, g, true);
+  for (int64_t c = 0; c < b.size(); ++c) geo[c] = (int8_t)g[c];
+}
+
+int lbmh_coronary_ends(int nx, int ny, int nz, lbmh_end* ends) {
+  // the windows of coronary.cu:75-143; they need x up to 273, y up to 200 and z up to 205
+  if (nx < 274 || ny < 201 || nz < 206) return -1;
+  ends[0] = lbmh_end{0, 3, 1, ny - 1, 1, nz - 1, 1};      // inlet end = 2
+  ends[1] = lbmh_end{0, 272, 1, ny - 1, 1, nz - 1, 2};    // main exit end = 3
+  ends[2] = lbmh_end{2, 185, 217, 237, 113, 138, 4};      // sub exit 1 = 5 (x 217..236, y 113..137)
+  ends[3] = lbmh_end{2, 191, 160, 206, 159, 200, 5};      // sub exit 2 = 6 (x 160..205, y 159..199)
+  ends[4] = lbmh_end{2, 204, 1, nx - 1, 1, ny - 1, 6};    // sub exit 3 = 7 (whole plane)
+  return 5;
+}
+
 long lbmh_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* geo, int inlet_block,
                       float* inlet_uy, float* outlet_uy) {
   FILE* f = std::fopen(path, "r");
@@ -197,6 +256,13 @@ void lbmh_initial_fields(int case_kind, int nx, int ny, int nz, const int8_t* ge
       for (int z = 0; z < nz; ++z)
         for (int x = 0; x < nx; ++x)
           if (geo[b(x, y, z)] != 0) uy[b(x, y, z)] = prof[x + (size_t)z * nx];
+  } else if (case_kind == 3) {
+    const float C_U = 2.74909090909091f;  // coronary.cu:20, 298-307 (float quotients)
+    for (int64_t c = 0; c < n; ++c) {
+      if (geo[c] == 2) ux[c] = 0.1745f / C_U;
+      if (geo[c] == 3) ux[c] = 0.1f / C_U;
+      if (geo[c] >= 5 && geo[c] <= 7) uz[c] = 0.02f / C_U;
+    }
   } else {
     for (int z = 0; z < nz; ++z)
       for (int x = 0; x < nx; ++x) {
@@ -253,20 +319,79 @@ int lbmh_write_vtk(const char* path, int case_kind, int nx, int ny, int nz, cons
   return ofs.good() ? 0 : -2;
 }
 
-long double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
-                     const float* uz) {
+int lbmh_write_vtk_coronary(const char* path, int nx, int ny, int nz, const int8_t* geo, const float* rho,
+                            const float* ux, const float* uy, const float* uz, float C_U, float CH, float C_rho) {
+  std::ofstream ofs(path);
+  if (!ofs) return -1;
+  const Box b{nx, ny, nz};
+  const float C_pre = C_rho * C_U * C_U;  // coronary.cu:26
+  ofs << "# vtk DataFile Version 2.0" << std::endl;
+  ofs << "<-- LBM flow with UIV acceleration, http://www.bg.ic.ac.uk/research/m.tang/ulis/ -->" << std::endl;
+  ofs << "ASCII" << std::endl;
+  ofs << "DATASET STRUCTURED_POINTS" << std::endl;
+  ofs << "DIMENSIONS " << nx - 2 << ' ' << ny - 4 << ' ' << nz - 2 << std::endl;
+  ofs << "SPACING " << CH << ' ' << CH << ' ' << CH << std::endl;
+  ofs << "ORIGIN " << std::round(nx / 2) * CH << ' ' << std::round(ny / 2) * CH << ' ' << .0 << std::endl;
+  ofs << "POINT_DATA  " << (nx - 2) * (ny - 4) * (nz - 2) << std::endl;
+  // one scalar section per quantity, region x in [1, nx-2], y in [2, ny-3], z in [1, nz-2]
+  auto region = [&](auto&& cell) {
+    for (int z = 1; z < nz - 1; ++z)
+      for (int y = 2; y < ny - 2; ++y)
+        for (int x = 1; x < nx - 1; ++x) cell(b(x, y, z));
+  };
+  ofs << "SCALARS DENSITY float" << std::endl;
+  ofs << "LOOKUP_TABLE default" << std::endl;
+  region([&](int64_t c) {
+    if (geo[c] != 0) ofs << rho[c] * C_rho << ' ';
+    else ofs << 0.0f << ' ';
+  });
+  ofs << std::endl;
+  ofs << "SCALARS PRESSURE float" << std::endl;
+  ofs << "LOOKUP_TABLE default" << std::endl;
+  region([&](int64_t c) {
+    if (geo[c] != 0) ofs << rho[c] * C_pre / 3.0 << ' ';
+    else ofs << 0.0f << ' ';
+  });
+  ofs << std::endl;
+  ofs << "VECTORS VELOCITY float" << std::endl;
+  region([&](int64_t c) {
+    if (geo[c] != 0) {
+      ofs << ux[c] * C_U << ' ';
+      ofs << uy[c] * C_U << ' ';
+      ofs << uz[c] * C_U << ' ';
+    } else {
+      ofs << 0 << ' ';
+      ofs << 0 << ' ';
+      ofs << 0 << ' ';
+    }
+  });
+  return ofs.good() ? 0 : -2;
+}
+
+static long double calc_res_codes(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
+                                  const float* uz, int lo, int hi) {
   const Box b{nx, ny, nz};
   long double s = 0.0L;
   for (int z = 1; z < nz - 1; ++z)
     for (int y = 2; y < ny - 2; ++y)
       for (int x = 1; x < nx - 1; ++x) {
         const int64_t c = b(x, y, z);
-        if (geo[c] >= 4) {
+        if (geo[c] >= lo && geo[c] <= hi) {
           const float v = ux[c] * ux[c] + uy[c] * uy[c] + uz[c] * uz[c];
           s = s + v;
         }
       }
   return s;
+}
+
+long double lbmh_calc_res(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
+                          const float* uz) {
+  return calc_res_codes(nx, ny, nz, geo, ux, uy, uz, 4, 127);
+}
+
+long double lbmh_calc_res_fluid(int nx, int ny, int nz, const int8_t* geo, const float* ux, const float* uy,
+                                const float* uz) {
+  return calc_res_codes(nx, ny, nz, geo, ux, uy, uz, 4, 4);
 }
 
 }  // extern "C"

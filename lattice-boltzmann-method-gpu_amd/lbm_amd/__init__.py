@@ -91,7 +91,13 @@ LBM_SYMBOLS = [
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
     "lbmh_index_transform", "lbmh_poiseuille_profile", "lbmh_initial_fields", "lbmh_write_vtk", "lbmh_calc_res",
+    "lbmh_read_geo_txt_zxy", "lbmh_geo_ends", "lbmh_coronary_ends", "lbmh_write_vtk_coronary", "lbmh_calc_res_fluid",
 ]
+
+
+class lbmh_end(C.Structure):
+    """include/lbm_host.h lbmh_end: one open end of a vessel mask (coronary.cu:75-143)."""
+    _fields_ = [(n, C.c_int) for n in ("axis", "plane", "lo0", "hi0", "lo1", "hi1", "passes")]
 
 _lbm = None
 _host = None
@@ -129,6 +135,12 @@ def host_lib() -> C.CDLL:
             "lbmh_write_vtk": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p,
                                          C.c_float, C.c_float]),
             "lbmh_calc_res": (C.c_longdouble, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
+            "lbmh_read_geo_txt_zxy": (C.c_long, [C.c_char_p, C.c_int, C.c_int, C.c_int, i32p]),
+            "lbmh_calc_res_fluid": (C.c_longdouble, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
+            "lbmh_geo_ends": (None, [C.c_int, C.c_int, C.c_int, i32p, C.c_int, C.POINTER(lbmh_end), i8p]),
+            "lbmh_coronary_ends": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(lbmh_end)]),
+            "lbmh_write_vtk_coronary": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p, f32p,
+                                                  C.c_float, C.c_float, C.c_float]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -241,6 +253,47 @@ def geo_mask(raw: np.ndarray) -> np.ndarray:
     g = np.zeros(raw.shape, np.int8)
     host_lib().lbmh_geo_mask(nx, ny, nz, _ptr(raw, C.c_int32), _ptr(g, C.c_int8))
     return g
+
+
+def read_geo_txt_zxy(path: str, shape) -> np.ndarray:
+    """coronary.cu:45-56: geo.txt in z, x, y loop order; returns the raster [nz][ny][nx]."""
+    nz, ny, nx = shape
+    raw = np.zeros(shape, np.int32)
+    n = host_lib().lbmh_read_geo_txt_zxy(path.encode(), nx, ny, nz, _ptr(raw, C.c_int32))
+    if n != raw.size:
+        raise LbmError(f"{path}: read {n} of {raw.size} mask values")
+    return raw
+
+
+def coronary_ends(shape):
+    """The reference's five vessel ends for a box of this shape (lbmh_coronary_ends) as tuples
+    (axis, plane, lo0, hi0, lo1, hi1, passes)."""
+    nz, ny, nx = shape
+    arr = (lbmh_end * 5)()
+    if host_lib().lbmh_coronary_ends(nx, ny, nz, arr) != 5:
+        raise LbmError(f"box {nx}x{ny}x{nz} cannot hold coronary.cu's end planes (needs >= 274x201x206)")
+    return [tuple(getattr(e, f) for f, _ in lbmh_end._fields_) for e in arr]
+
+
+def geo_ends(raw: np.ndarray, ends) -> np.ndarray:
+    """geo_pre of a vessel mask with open ends (lbmh_geo_ends, coronary.cu:31-275)."""
+    raw = np.ascontiguousarray(raw, np.int32)
+    nz, ny, nx = raw.shape
+    arr = (lbmh_end * max(1, len(ends)))(*[lbmh_end(*e) for e in ends])
+    g = np.zeros(raw.shape, np.int8)
+    host_lib().lbmh_geo_ends(nx, ny, nz, _ptr(raw, C.c_int32), len(ends), arr, _ptr(g, C.c_int8))
+    return g
+
+
+def write_vtk_coronary(path: str, geo: np.ndarray, rho, ux, uy, uz, C_U: float = 2.74909090909091,
+                       CH: float = 6.1111e-05, C_rho: float = 1060.0) -> None:
+    g = np.ascontiguousarray(geo, np.int8)
+    nz, ny, nx = g.shape
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (rho, ux, uy, uz)]
+    rc = host_lib().lbmh_write_vtk_coronary(path.encode(), nx, ny, nz, _ptr(g, C.c_int8),
+                                            *[_ptr(a, C.c_float) for a in arrs], C_U, CH, C_rho)
+    if rc != 0:
+        raise LbmError(f"cannot write {path}")
 
 
 def read_bc_txt(path: str, geo, inlet_block: int = 0):

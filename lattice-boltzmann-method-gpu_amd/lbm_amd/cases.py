@@ -175,3 +175,55 @@ def coronary_bc_codes(c_u: float = 2.74909090909091):
              {"code": 3, "face": LBM_FACE_NX, "kind": LBM_BC_VELOCITY, "u": (uout, 0.0, 0.0)}]
     codes += [{"code": k, "face": LBM_FACE_NZ, "kind": LBM_BC_VELOCITY, "u": (0.0, 0.0, uz)} for k in (5, 6, 7)]
     return codes
+
+
+# coronary_cfd/coronary.cu: box, relaxation time and output constants (coronary.cu:19-20, 23, 357)
+CORONARY_SHAPE = (372, 291, 291)  # (nz, ny, nx)
+CORONARY_TAU = 0.55
+CORONARY_C_U, CORONARY_CH, CORONARY_C_RHO = 2.74909090909091, 6.1111e-05, 1060.0
+
+
+def vessel_mask(shape, tube, branches):
+    """A synthetic vessel tree as a raw 0/1 mask (the reference's coronary geo.txt is not shipped):
+    tube = (x0, x1, yc, zc, r): a main vessel along x over [x0, x1] with a circular cross-section;
+    branches = [(xc, yc, z0, z1, r)]: vessels along z over [z0, z1].  Open ends sit where a
+    vessel stops: the planes x = x0, x = x1 and z = z1 of each branch."""
+    nz, ny, nx = shape
+    raw = np.zeros(shape, np.int32)
+    z, y, x = np.ogrid[:nz, :ny, :nx]
+    x0, x1, yc, zc, r = tube
+    raw[((y - yc) ** 2 + (z - zc) ** 2 <= r * r) & (x >= x0) & (x <= x1)] = 1
+    for xc, byc, z0, z1, br in branches:
+        raw[((x - xc) ** 2 + (y - byc) ** 2 <= br * br) & (z >= z0) & (z <= z1)] = 1
+    return raw
+
+
+def coronary_reference_vessel():
+    """A vessel tree in the reference's 291 x 291 x 372 box whose open ends lie on coronary.cu's
+    five end planes, inside their windows: main vessel x = 3 .. 272 (inlet, main exit), branches
+    ending at z = 185 (window x 217..236, y 113..137), 191 (x 160..205, y 159..199) and 204."""
+    return vessel_mask(CORONARY_SHAPE, (3, 272, 150, 60, 30),
+                       [(227, 125, 60, 185, 6), (183, 179, 60, 191, 8), (100, 150, 60, 204, 10)])
+
+
+def coronary_small_vessel():
+    """A small vessel tree with its own end table (same roles and pass counts as coronary.cu's
+    ends): inlet x = 3, main exit x = 50, branches ending at z = 30 / 33 (windows) and z = 36
+    (whole plane).  Returns (raw, ends)."""
+    shape = (40, 28, 56)
+    raw = vessel_mask(shape, (3, 50, 14, 12, 8), [(20, 14, 12, 30, 3), (36, 12, 12, 33, 3), (44, 16, 12, 36, 3)])
+    nz, ny, nx = shape
+    ends = [(0, 3, 1, ny - 1, 1, nz - 1, 1), (0, 50, 1, ny - 1, 1, nz - 1, 2), (2, 30, 15, 26, 9, 20, 4),
+            (2, 33, 31, 42, 7, 18, 5), (2, 36, 1, nx - 1, 1, ny - 1, 6)]
+    return raw, ends
+
+
+def coronary(raw: np.ndarray, ends=None, device: int = 0, tau: float = CORONARY_TAU):
+    """coronary.cu's set-up as a LBM_CASE_GENERIC lattice: geo_pre of the raw vessel mask with
+    its open ends (the reference's five for its box by default), the coronary boundary codes
+    (coronary_bc_codes) and initialize()'s state (coronary.cu:277-350).  Returns (lat, geo)."""
+    from . import LBM_CASE_GENERIC, coronary_ends, geo_ends
+    geo = geo_ends(raw, coronary_ends(raw.shape) if ends is None else ends)
+    lat = Lattice(LBM_CASE_GENERIC, geo.shape, tau, geo, device=device, bc_codes=coronary_bc_codes())
+    lat.init_equilibrium(LBM_INIT_EXPANDED, *initial_fields(3, geo))
+    return lat, geo

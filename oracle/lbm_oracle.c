@@ -181,6 +181,73 @@ void orc_geo_mask(int nx, int ny, int nz, const int32_t* raw, int8_t* geo) {
     free(g);
 }
 
+/* coronary.cu:45-56: the same token stream, loop z, x, y (y fastest) */
+int orc_read_geo_txt_zxy(const char* path, int nx, int ny, int nz, int32_t* raw) {
+    FILE* f = fopen(path, "r");
+    if (!f) return -1;
+    int i = 0, v;
+    for (int z = 0; z < nz; z++)
+        for (int x = 0; x < nx; x++)
+            for (int y = 0; y < ny; y++) {
+                if (fscanf(f, "%d ", &v) != 1) { fclose(f); return i; }
+                raw[x + (long)nx * (y + (long)ny * z)] = v;
+                i++;
+            }
+    fclose(f);
+    return i;
+}
+
+/* coronary.cu:31-275 (geo_pre).  The reference hard-codes five end planes for its
+ * 291 x 291 x 372 box (75-143); here each end is ends[7 e .. 7 e + 6] =
+ * {axis (0 = x plane, 2 = z plane), plane, lo0, hi0, lo1, hi1, passes}, looped as the
+ * reference loops them: x planes over y in [lo0, hi0) outer, z in [lo1, hi1) inner, with the
+ * y and z neighbours (75-99); z planes over [lo0, hi0) x [lo1, hi1) with the y and x
+ * neighbours (101-143). */
+void orc_geo_coronary(int nx, int ny, int nz, const int32_t* raw, int n_ends, const int* ends, int8_t* geo) {
+    long n = (long)nx * ny * nz;
+    int* g = (int*)calloc((size_t)n, sizeof(int));
+    for (long c = 0; c < n; c++) g[c] = raw[c]; /* 45-56: h_geo = flag = tmp */
+#define F(x, y, z) raw[(x) + (long)nx * ((y) + (long)ny * (z))]
+#define G(x, y, z) g[(x) + (long)nx * ((y) + (long)ny * (z))]
+    /* 58-73: distance transform, fluid = 4 */
+    for (int t = 0; t < 3; t++)
+        for (int x = 1; x < nx - 1; x++)
+            for (int y = 1; y < ny - 1; y++)
+                for (int z = 1; z < nz - 1; z++) {
+                    int minx = imin(F(x + 1, y, z), F(x - 1, y, z));
+                    int miny = imin(F(x, y - 1, z), F(x, y + 1, z));
+                    int minz = imin(F(x, y, z - 1), F(x, y, z + 1));
+                    G(x, y, z) = G(x, y, z) + imin(imin(minx, miny), minz);
+                }
+    for (int e = 0; e < n_ends; e++) {
+        const int* E = ends + 7 * e;
+        for (int t = 0; t < E[6]; t++) {
+            if (E[0] == 0) { /* 75-99: x = plane, y outer, z inner */
+                int x = E[1];
+                for (int y = E[2]; y < E[3]; y++)
+                    for (int z = E[4]; z < E[5]; z++) {
+                        int miny = imin(F(x, y - 1, z), F(x, y + 1, z));
+                        int minz = imin(F(x, y, z - 1), F(x, y, z + 1));
+                        G(x, y, z) = G(x, y, z) + imin(miny, minz);
+                    }
+            } else { /* 101-143: z = plane; the window's first range is x, the second y */
+                int z = E[1];
+                for (int x = E[2]; x < E[3]; x++)
+                    for (int y = E[4]; y < E[5]; y++) {
+                        int miny = imin(F(x, y - 1, z), F(x, y + 1, z));
+                        int minz = imin(F(x - 1, y, z), F(x + 1, y, z)); /* the reference's name */
+                        G(x, y, z) = G(x, y, z) + imin(miny, minz);
+                    }
+            }
+        }
+    }
+#undef F
+#undef G
+    for (long c = 0; c < n; c++) geo[c] = (int8_t)g[c];
+    mark_ghosts(nx, ny, nz, geo, 0); /* 145-260: around geo == 1 */
+    free(g);
+}
+
 /* bifurcation.cu:294-325 */
 int orc_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* geo, int skip_blocks,
                     float* inlet_uy, float* outlet_uy) {
@@ -441,6 +508,28 @@ void orc_initialize(orc_lbm* o) {
     o->sum_current = 0.0f;
     memset(o->rho, 0, sizeof(float) * n); memset(o->ux, 0, sizeof(float) * n);
     memset(o->uy, 0, sizeof(float) * n); memset(o->uz, 0, sizeof(float) * n);
+}
+
+/* coronary.cu:277-350 (initialize) for a generic instance holding the coronary codes: every
+ * stored cell rho = 1, u = 0; code 2 u_x = 0.1745f/C_U, 3 u_x = 0.1f/C_U, 5/6/7 u_z = 0.02f/C_U
+ * (float quotients; the boundary kernel's are double, coronary.cu:717, 797), then the update-form
+ * equilibrium (309-348, the same expression trees as feq_update). */
+void orc_initialize_coronary(orc_lbm* o) {
+    const long n = o->ncell;
+    const float C_U = 2.74909090909091f;
+    float feq[19];
+    for (long c = 0; c < n; c++) {
+        int g = o->geo[c];
+        if (g == 0) continue;
+        float ux = 0.0f, uy = 0.0f, uz = 0.0f;
+        if (g == 2) ux = 0.1745f / C_U;
+        if (g == 3) ux = 0.1f / C_U;
+        if (g == 5) uz = 0.02f / C_U;
+        if (g == 6) uz = 0.02f / C_U;
+        if (g == 7) uz = 0.02f / C_U;
+        feq_update(1.0f, ux, uy, uz, feq);
+        for (int q = 0; q < 19; q++) o->src[q * n + c] = o->dst[q * n + c] = feq[q];
+    }
 }
 
 static int fluid_code(const orc_lbm* o) { return o->kind == ORC_LDC ? 3 : 4; }

@@ -61,6 +61,10 @@ void orc_geo_ldc(int nx, int ny, int nz, int8_t* geo);                      /* l
 void orc_geo_poiseuille(int nx, int ny, int nz, int8_t* geo);               /* Poiseulle.cu:52-255 */
 void orc_geo_mask(int nx, int ny, int nz, const int32_t* raw, int8_t* geo); /* bifurcation.cu:36-253 */
 int  orc_read_geo_txt(const char* path, int n, int32_t* raw);               /* bifurcation.cu:50-60 */
+int  orc_read_geo_txt_zxy(const char* path, int nx, int ny, int nz, int32_t* raw); /* coronary.cu:45-56 */
+/* coronary.cu:31-275 with its five hard-coded ends as a table: ends[7e..7e+6] =
+ * {axis 0|2, plane, lo0, hi0, lo1, hi1, passes} (see lbm_oracle.c) */
+void orc_geo_coronary(int nx, int ny, int nz, const int32_t* raw, int n_ends, const int* ends, int8_t* geo);
 /* bifurcation.cu:255-327: fills inlet (y=1, geo==2) and outlet (y=ny-2, geo==3) uy tables,
  * skipping `skip_blocks` nx*nz blocks first (1 = the "inlet = block 1" variant). Returns tokens read. */
 int  orc_read_bc_txt(const char* path, int nx, int ny, int nz, const int8_t* geo, int skip_blocks,
@@ -75,6 +79,8 @@ orc_lbm* orc_create(int case_kind, int nx, int ny, int nz, const int8_t* geo, fl
  * listed boundary codes (at most 16), everything else unstored. */
 orc_lbm* orc_create_generic(int nx, int ny, int nz, const int8_t* geo, float tau, const orc_bc* bcs, int nbc);
 void orc_destroy(orc_lbm* o);
+/* coronary.cu:277-350: the coronary case's own initial state (after orc_create_generic) */
+void orc_initialize_coronary(orc_lbm* o);
 /* the update kernel's equilibrium (Poiseulle.cu:561-580 expression trees) */
 void orc_feq(float rho, float ux, float uy, float uz, float* feq19);
 /* the boundary-value equilibrium of the NEE "tmp" terms (fp32 throughout) */

@@ -45,6 +45,8 @@ def lib() -> C.CDLL:
             "orc_geo_poiseuille": (None, [C.c_int, C.c_int, C.c_int, i8p]),
             "orc_geo_mask": (None, [C.c_int, C.c_int, C.c_int, i32p, i8p]),
             "orc_read_geo_txt": (C.c_int, [C.c_char_p, C.c_int, i32p]),
+            "orc_read_geo_txt_zxy": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, i32p]),
+            "orc_geo_coronary": (None, [C.c_int, C.c_int, C.c_int, i32p, C.c_int, i32p, i8p]),
             "orc_read_bc_txt": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, i8p, C.c_int, f32p, f32p]),
             "orc_index_transform": (C.c_int, [C.c_int, C.c_int, C.c_int, i8p, i32p]),
             "orc_create": (P, [C.c_int, C.c_int, C.c_int, C.c_int, i8p, C.c_float, C.c_int, f32p, f32p]),
@@ -53,6 +55,7 @@ def lib() -> C.CDLL:
             "orc_feq": (None, [C.c_float, C.c_float, C.c_float, C.c_float, f32p]),
             "orc_feq_bc": (None, [C.c_float, C.c_float, C.c_float, C.c_float, f32p]),
             "orc_initialize": (None, [P]),
+            "orc_initialize_coronary": (None, [P]),
             "orc_step": (None, [P, C.c_int, f32p]),
             "orc_run_converge": (C.c_int, [P, C.c_int, C.c_int, C.c_float, f32p]),
             "orc_steps_done": (C.c_int, [P]),
@@ -101,6 +104,35 @@ def geo_mask(raw: np.ndarray) -> np.ndarray:
     raw = np.ascontiguousarray(raw, np.int32)
     g = np.zeros((nz, ny, nx), np.int8)
     lib().orc_geo_mask(nx, ny, nz, _p(raw, C.c_int32), _p(g, C.c_int8))
+    return g
+
+
+def read_geo_txt_zxy(path: str, nx: int, ny: int, nz: int) -> np.ndarray:
+    """coronary.cu:45-56: geo.txt in z, x, y loop order, returned as a raster [nz][ny][nx]."""
+    raw = np.zeros((nz, ny, nx), np.int32)
+    n = lib().orc_read_geo_txt_zxy(path.encode(), nx, ny, nz, _p(raw, C.c_int32))
+    if n != raw.size:
+        raise ValueError(f"{path}: read {n} of {raw.size} ints")
+    return raw
+
+
+def coronary_ends(nx: int, ny: int, nz: int):
+    """The five ends coronary.cu:75-143 hard-codes for its 291 x 291 x 372 box, as
+    (axis, plane, lo0, hi0, lo1, hi1, passes): x = 3 over y, z in [1, N-2] once (inlet, code 2);
+    x = 272 twice (3); z = 185 over x in [217, 237), y in [113, 138) four times (5); z = 191 over
+    x in [160, 206), y in [159, 200) five times (6); z = 204 over x, y in [1, N-2] six times (7)."""
+    return [(0, 3, 1, ny - 1, 1, nz - 1, 1), (0, 272, 1, ny - 1, 1, nz - 1, 2),
+            (2, 185, 217, 237, 113, 138, 4), (2, 191, 160, 206, 159, 200, 5),
+            (2, 204, 1, nx - 1, 1, ny - 1, 6)]
+
+
+def geo_coronary(raw: np.ndarray, ends) -> np.ndarray:
+    """coronary.cu:31-275 geo_pre with the end table `ends` (coronary_ends for the reference box)."""
+    nz, ny, nx = raw.shape
+    raw = np.ascontiguousarray(raw, np.int32)
+    e = np.ascontiguousarray(np.array(ends, np.int32).reshape(-1))
+    g = np.zeros((nz, ny, nx), np.int8)
+    lib().orc_geo_coronary(nx, ny, nz, _p(raw, C.c_int32), len(ends), _p(e, C.c_int32), _p(g, C.c_int8))
     return g
 
 
@@ -186,6 +218,10 @@ class Oracle:
     def set_f(self, f: np.ndarray) -> None:
         a = np.ascontiguousarray(f, np.float32)
         lib().orc_set_f(self.h, _p(a, C.c_float))
+
+    def initialize_coronary(self) -> None:
+        """Replace the generic initial state with coronary.cu:277-350's (float velocity quotients)."""
+        lib().orc_initialize_coronary(self.h)
 
     def bad_reads(self) -> int:
         return int(lib().orc_bad_reads(self.h))

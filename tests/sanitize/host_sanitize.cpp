@@ -1,0 +1,111 @@
+// ASan/UBSan exercise of the host-side C code: liblbm_host (lattice-boltzmann-method-gpu_amd/csrc/
+// lbm_host.cpp) and the oracle (oracle/lbm_oracle.c) compiled from source with
+// -fsanitize=address,undefined and driven through every entry point on small inputs, including
+// the shipped bifurcation geo.txt / bc.txt (argv[1], argv[2]) and a coronary-style vessel.
+// Built and run by tests/test_sanitizers.py; any sanitizer report aborts with a non-zero status.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../include/lbm_host.h"
+#include "../../oracle/lbm_oracle.h"
+
+static int fail(const char* what) {
+  std::fprintf(stderr, "FAIL %s\n", what);
+  return 1;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) return fail("usage: host_sanitize geo.txt bc.txt outdir");
+  const std::string out = argv[3];
+  // cases 0..2 on small boxes: host geometry equals the oracle's, one VTK each
+  for (int kind = 0; kind < 2; ++kind) {
+    const int nx = 13, ny = 17, nz = 11;
+    const size_t n = (size_t)nx * ny * nz;
+    std::vector<int8_t> g(n), go(n);
+    if (kind == 0) { lbmh_geo_ldc(nx, ny, nz, g.data()); orc_geo_ldc(nx, ny, nz, go.data()); }
+    else { lbmh_geo_poiseuille(nx, ny, nz, g.data()); orc_geo_poiseuille(nx, ny, nz, go.data()); }
+    if (g != go) return fail("geo");
+    std::vector<float> rho(n), ux(n), uy(n), uz(n);
+    lbmh_initial_fields(kind, nx, ny, nz, g.data(), nullptr, nullptr, rho.data(), ux.data(), uy.data(), uz.data());
+    orc_lbm* o = orc_create(kind, nx, ny, nz, g.data(), 0.56f, 0, nullptr, nullptr);
+    orc_initialize(o);
+    std::vector<float> hist(7);
+    orc_step(o, 7, hist.data());
+    orc_get_macros(o, rho.data(), ux.data(), uy.data(), uz.data());
+    orc_destroy(o);
+    if (lbmh_write_vtk((out + "/k" + std::to_string(kind) + ".vtk").c_str(), kind, nx, ny, nz, g.data(), ux.data(),
+                       uy.data(), uz.data(), 1.5f, 1e-4f) != 0)
+      return fail("vtk");
+  }
+  // bifurcation: the shipped files
+  {
+    const int nx = 64, ny = 83, nz = 32;
+    const size_t n = (size_t)nx * ny * nz;
+    std::vector<int32_t> raw(n);
+    if (lbmh_read_geo_txt(argv[1], nx, ny, nz, raw.data()) != (long)n) return fail("geo.txt");
+    std::vector<int8_t> g(n), go(n);
+    lbmh_geo_mask(nx, ny, nz, raw.data(), g.data());
+    orc_geo_mask(nx, ny, nz, raw.data(), go.data());
+    if (g != go) return fail("geo_mask");
+    std::vector<float> in((size_t)nx * nz), outl((size_t)nx * nz);
+    if (lbmh_read_bc_txt(argv[2], nx, ny, nz, g.data(), 1, in.data(), outl.data()) <= 0) return fail("bc.txt");
+    std::vector<int32_t> idx(n);
+    if (lbmh_index_transform(nx, ny, nz, g.data(), idx.data()) != 65820) return fail("NLATTICE");
+    std::vector<float> rho(n), ux(n), uy(n), uz(n);
+    lbmh_initial_fields(2, nx, ny, nz, g.data(), in.data(), outl.data(), rho.data(), ux.data(), uy.data(), uz.data());
+    orc_lbm* o = orc_create(ORC_MASK, nx, ny, nz, g.data(), 0.55f, 0, in.data(), outl.data());
+    orc_initialize(o);
+    orc_step(o, 5, nullptr);
+    orc_get_macros(o, rho.data(), ux.data(), uy.data(), uz.data());
+    orc_destroy(o);
+    const long double s = lbmh_calc_res(nx, ny, nz, g.data(), ux.data(), uy.data(), uz.data());
+    if (!(s >= 0.0L)) return fail("calc_res");
+    if (lbmh_write_vtk((out + "/bif.vtk").c_str(), 2, nx, ny, nz, g.data(), ux.data(), uy.data(), uz.data(), 0.24f,
+                       2e-4f) != 0)
+      return fail("vtk bif");
+  }
+  // coronary-style vessel: ends, generic NEE, three-section VTK
+  {
+    const int nx = 30, ny = 20, nz = 24;
+    const size_t n = (size_t)nx * ny * nz;
+    std::vector<int32_t> raw(n, 0);
+    for (int z = 0; z < nz; ++z)
+      for (int y = 0; y < ny; ++y)
+        for (int x = 0; x < nx; ++x) {
+          const bool tube = (y - 10) * (y - 10) + (z - 8) * (z - 8) <= 25 && x >= 3 && x <= 25;
+          const bool branch = (x - 14) * (x - 14) + (y - 10) * (y - 10) <= 4 && z >= 8 && z <= 18;
+          raw[x + (size_t)nx * (y + (size_t)ny * z)] = tube || branch;
+        }
+    const lbmh_end ends[3] = {{0, 3, 1, ny - 1, 1, nz - 1, 1}, {0, 25, 1, ny - 1, 1, nz - 1, 2},
+                              {2, 18, 1, nx - 1, 1, ny - 1, 4}};
+    const int eo[21] = {0, 3, 1, ny - 1, 1, nz - 1, 1, 0, 25, 1, ny - 1, 1, nz - 1, 2, 2, 18, 1, nx - 1, 1, ny - 1, 4};
+    std::vector<int8_t> g(n), go(n);
+    lbmh_geo_ends(nx, ny, nz, raw.data(), 3, ends, g.data());
+    orc_geo_coronary(nx, ny, nz, raw.data(), 3, eo, go.data());
+    if (g != go) return fail("geo_ends");
+    lbmh_end ref[5];
+    if (lbmh_coronary_ends(nx, ny, nz, ref) != -1 || lbmh_coronary_ends(291, 291, 372, ref) != 5) return fail("ends");
+    std::vector<float> rho(n), ux(n), uy(n), uz(n);
+    lbmh_initial_fields(3, nx, ny, nz, g.data(), nullptr, nullptr, rho.data(), ux.data(), uy.data(), uz.data());
+    orc_bc bcs[3] = {{2, 0, 1, 1.0f, {0.06f, 0.0f, 0.0f}, nullptr}, {3, 1, 0, 1.0f, {0.03f, 0.0f, 0.0f}, nullptr},
+                     {5, 5, 0, 1.0f, {0.0f, 0.0f, 0.01f}, nullptr}};
+    orc_lbm* o = orc_create_generic(nx, ny, nz, g.data(), 0.55f, bcs, 3);
+    orc_initialize(o);
+    orc_initialize_coronary(o);
+    orc_step(o, 9, nullptr);
+    orc_get_macros(o, rho.data(), ux.data(), uy.data(), uz.data());
+    if (orc_bad_reads(o) != 0) return fail("bad reads");
+    orc_destroy(o);
+    (void)lbmh_calc_res_fluid(nx, ny, nz, g.data(), ux.data(), uy.data(), uz.data());
+    if (lbmh_write_vtk_coronary((out + "/cor.vtk").c_str(), nx, ny, nz, g.data(), rho.data(), ux.data(), uy.data(),
+                                uz.data(), 2.75f, 6e-5f, 1060.f) != 0)
+      return fail("vtk coronary");
+    std::vector<int32_t> r2(n);
+    if (lbmh_read_geo_txt_zxy((out + "/missing.txt").c_str(), nx, ny, nz, r2.data()) != -1) return fail("missing");
+  }
+  std::printf("sanitize ok\n");
+  return 0;
+}
