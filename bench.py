@@ -296,8 +296,9 @@ def main():
             "stream_probe_gbs": probe,
             "frac_of_stream_probe": round(achieved / probe, 4) if probe else None,
             "stream_probe": "lbm_probe_stream: best of 7 streaming-copy shapes (16-B vectors, grid-stride or "
-                            "per-XCD regions, plain or non-temporal; read + write bytes / time) of 2 x 8 GiB "
-                            "on this GPU in this run",
+                            "per-XCD regions, plain or non-temporal; read + write bytes / time) between the two "
+                            "fastest-writing of up to six 8-GiB allocations (the population buffers' placement "
+                            "rule) on this GPU in this run",
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
         "step_kernel_ms_by_source_buffer": parity_ms,

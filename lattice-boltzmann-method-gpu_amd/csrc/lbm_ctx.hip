@@ -1315,12 +1315,48 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   double best = 0.0;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipMalloc(&a, n4 * 16);
-  if (e == hipSuccess) e = hipMalloc(&b, n4 * 16);
-  if (e == hipSuccess) e = hipMemset(a, 0x3c, n4 * 16);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
+  // the same placement rule as the population buffers (buffer_placement): an allocation
+  // sweep-writes at ~6.4 or ~5.5 TB/s for its lifetime, so up to six candidates are timed over
+  // one write sweep each and the copies run between the two fastest
+  {
+    std::vector<void*> cand;
+    std::vector<double> rate;
+    size_t fr = 0, tot = 0;
+    if (e == hipSuccess) e = hipMemGetInfo(&fr, &tot);
+    const size_t sz = (size_t)n4 * 16;
+    const int ncand = (int)std::max<size_t>(2, std::min<size_t>(6, fr > sz ? (fr - sz) / sz : 0));
+    for (int i = 0; i < ncand && e == hipSuccess; ++i) {
+      void* q = nullptr;
+      e = hipMalloc(&q, sz);
+      if (e != hipSuccess) break;
+      cand.push_back(q);
+      e = hipMemsetAsync(q, 0x3c, sz, st);
+      if (e == hipSuccess) e = launch_probe_fill(q, n4, st);  // warm-up sweep
+      if (e == hipSuccess) e = hipEventRecord(e0, st);
+      if (e == hipSuccess) e = launch_probe_fill(q, n4, st);
+      if (e == hipSuccess) e = hipEventRecord(e1, st);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      float ms = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      rate.push_back(ms > 0.f ? (double)sz / ms : 0.0);
+    }
+    if (e == hipErrorOutOfMemory && cand.size() >= 2) {
+      (void)hipGetLastError();
+      e = hipSuccess;
+    }
+    std::vector<int> order(cand.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return rate[x] > rate[y]; });
+    for (size_t k = 0; k < order.size(); ++k) {
+      if (e == hipSuccess && k == 0) a = cand[order[k]];
+      else if (e == hipSuccess && k == 1) b = cand[order[k]];
+      else (void)hipFree(cand[order[k]]);
+    }
+    if (e == hipSuccess && (!a || !b)) e = hipErrorOutOfMemory;
+  }
   const int shapes[][2] = {{8192, 0}, {8192, 1}, {8192, 2}, {8192, 3}, {4096, 4}, {2048, 5}, {32768, 2}};
   for (const auto& sh : shapes) {  // blocks, launch_probe_copy shape
     if (e != hipSuccess) break;
