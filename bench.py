@@ -295,8 +295,8 @@ def main():
             "boundary_cells_per_gpu": counts["n_boundary"],
             "stream_probe_gbs": probe,
             "frac_of_stream_probe": round(achieved / probe, 4) if probe else None,
-            "stream_probe": "lbm_probe_stream: best of 7 streaming-copy shapes (16-B vectors, grid-stride or "
-                            "per-XCD regions, plain or non-temporal; read + write bytes / time) between the two "
+            "stream_probe": "lbm_probe_stream: best of 9 streaming-copy shapes (16-B vectors, grid-stride, "
+                            "per-XCD regions or k_step-like 16-KB wave tiles, plain or non-temporal; read + write bytes / time) between the two "
                             "fastest-writing of up to six 8-GiB allocations (the population buffers' placement "
                             "rule) on this GPU in this run",
         },

@@ -251,7 +251,8 @@ int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
 /* Measurement helper (not a reference interface): the HBM rate a plain streaming copy
  * reaches on this device, for context next to k_step's roofline fraction.  Copies `bytes`
  * (rounded down to 64 KiB) between two device buffers with 16-B loads and stores in a few
- * shapes (grid-stride or one contiguous region per XCD, plain or non-temporal), `reps` timed
+ * shapes (grid-stride or one contiguous region per XCD, plain or non-temporal, and k_step's own:
+ * one wave per 16-KB tile with all 16 loads per lane in flight), `reps` timed
  * launches each (HIP events, after one untimed launch); *gbs = the best (read + write bytes) /
  * duration in GB/s.  The two buffers are picked as the population buffers are
  * (lbm_buffer_placement): the two fastest-writing of up to six allocations of `bytes`. */

@@ -1357,7 +1357,7 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
     }
     if (e == hipSuccess && (!a || !b)) e = hipErrorOutOfMemory;
   }
-  const int shapes[][2] = {{8192, 0}, {8192, 1}, {8192, 2}, {8192, 3}, {4096, 4}, {2048, 5}, {32768, 2}};
+  const int shapes[][2] = {{8192, 0}, {8192, 1}, {8192, 2}, {8192, 3}, {4096, 4}, {2048, 5}, {32768, 2}, {0, 6}, {0, 7}};
   for (const auto& sh : shapes) {  // blocks, launch_probe_copy shape
     if (e != hipSuccess) break;
     e = launch_probe_copy(a, b, n4, sh[0], sh[1], st);  // untimed first launch

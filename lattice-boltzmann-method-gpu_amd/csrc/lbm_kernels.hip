@@ -1136,10 +1136,36 @@ __global__ __launch_bounds__(256) void k_probe_copy(const f4* __restrict__ a, f4
   }
 }
 
+// k_step's own access shape: one wave per 16-KB tile, its 16 loads per lane (256 B) all in
+// flight before the first store, tiles dealt to the XCDs in contiguous runs (k_step's chunk order)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_probe_tiles(const f4* __restrict__ a, f4* __restrict__ b, int64_t ntiles) {
+  const int64_t nb = gridDim.x;  // a multiple of 8
+  const int64_t lb = (int64_t)(blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+  const int64_t tile = lb * 4 + (threadIdx.x >> 6);
+  if (tile >= ntiles) return;
+  const int64_t base = tile * 1024 + (threadIdx.x & 63);
+  f4 v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = NT ? __builtin_nontemporal_load(a + base + k * 64) : a[base + k * 64];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if constexpr (NT) __builtin_nontemporal_store(v[k], b + base + k * 64);
+    else b[base + k * 64] = v[k];
+  }
+}
+
 hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks, int shape, hipStream_t s) {
   const f4* a = static_cast<const f4*>(src);
   f4* b = static_cast<f4*>(dst);
   blocks = blocks / 8 * 8;
+  if (shape >= 6) {  // tiles: n4 is a whole number of 64-KiB blocks, i.e. of 4-tile workgroups
+    const int64_t ntiles = n4 / 1024;
+    const unsigned grid = (unsigned)((ntiles / 4 + 7) / 8 * 8);
+    if (shape == 6) hipLaunchKernelGGL((k_probe_tiles<true>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
+    else hipLaunchKernelGGL((k_probe_tiles<false>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
+    return hipGetLastError();
+  }
   switch (shape) {
     case 0: hipLaunchKernelGGL((k_probe_copy<1, false, true>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
     case 1: hipLaunchKernelGGL((k_probe_copy<1, false, false>), dim3(blocks), dim3(256), 0, s, a, b, n4); break;
