@@ -15,15 +15,42 @@ pytestmark = pytest.mark.gpu
 BIN = os.path.join(PKG, "bin")
 
 
-def _oracle_vtk(lbm, oracle, geo, steps, path, kind, C_U, CH, **kw):
-    o = oracle.Oracle(kind, geo, kw.pop("tau"), **kw)
-    o.step(steps)
-    rho, ux, uy, uz = o.macros()
-    lbm.write_vtk(path, {oracle.LDC: 0, oracle.POISEUILLE: 1, oracle.MASK: 2}[kind], geo, ux, uy, uz, C_U, CH)
-    return open(path).read()
+def _vtk_ldc_independent(nx, ny, nz, ux, uy, uz, C_U, CH):
+    """ldc.cu:582-610 outputSave written here from the reference text (not lbmh_write_vtk):
+    every cell of x, y, z in [2, n-3], u * C_U in fp32, C++ ostream default formatting (%g)."""
+    f32 = np.float32
+    lines = ["# vtk DataFile Version 2.0",
+             "<-- LBM flow with UIV acceleration, http://www.bg.ic.ac.uk/research/m.tang/ulis/ -->",
+             "ASCII", "DATASET STRUCTURED_POINTS",
+             f"DIMENSIONS {nx - 4} {ny - 4} {nz - 4}",
+             "SPACING {0:g} {0:g} {0:g}".format(float(f32(CH))),
+             "ORIGIN {:g} {:g} {:g}".format(float(nx // 2 - 1) * float(f32(CH)), float(ny // 2 - 1) * float(f32(CH)),
+                                           0.0),
+             f"POINT_DATA  {(nx - 4) * (ny - 4) * (nz - 4)}",
+             "VECTORS VELOCITY float"]
+    sl = (slice(2, nz - 2), slice(2, ny - 2), slice(2, nx - 2))
+    cu = f32(C_U)
+    vals = np.stack([(a[sl] * cu).astype(np.float32) for a in (ux, uy, uz)], axis=-1)
+    return "\n".join(lines) + "\n" + "".join("%g " % v for v in vals.reshape(-1).astype(np.float64))
+
+
+def _oracle_run(oracle, kind, geo, tau, steps):
+    """The oracle after each step count in `steps` (ascending): (macros, fp32 residual history of
+    every step so far), with the |u| sum in fp64 as liblbm sums it (oracle/PINNING.md section 3)."""
+    o = oracle.Oracle(kind, geo, tau)
+    o.residual_fp64(True)
+    hist, done, out = [], 0, {}
+    for s in steps:
+        hist.extend(o.step(s - done))
+        done = s
+        out[s] = o.macros()
+    return out, np.array(hist, np.float32)
 
 
 def test_ldc_driver(gpu, oracle, tmp_path):
+    """bin/ldc (ldc.cu main): snapshots lid_<k>.vtk at k % time_save == 0 and after the loop, the
+    printed and logged residuals (ldc.cu:668-691) -- all against the oracle's fields and fp64-sum
+    residual history, the VTK rendered by an independent writer."""
     n, max_it, save = 24, 25, 10
     out = tmp_path / "out"
     r = subprocess.run([os.path.join(BIN, "ldc"), "--nx", str(n), "--ny", str(n), "--nz", str(n), "--max-it",
@@ -33,30 +60,38 @@ def test_ldc_driver(gpu, oracle, tmp_path):
     assert re.fullmatch(r"ITERATION # 0, collapse time: [0-9.e+-]+ ms, residual:[0-9.e+-]+", lines[0])
     assert [int(re.search(r"# (\d+),", x).group(1)) for x in lines if x.startswith("ITERATION")] == [0, 10, 20]
     assert re.fullmatch(r"TOTAL RUNNING TIME: [0-9.e+-]+ MILLI SECONDS#LATTICE\d+", lines[-2])
-    assert lines[-1].startswith("Residual is ")
     log = (out / "CONVERGENCE.log").read_text().strip().splitlines()
-    assert len(log) == 4 and log[-1].startswith("TOTAL RUNNING TIME:") and " ERROR IS" in log[-1]
+    assert len(log) == 4 and log[-1].startswith("TOTAL RUNNING TIME:")
     geo = gpu.geo_ldc(n, n, n)
     C_U, CH = 2.4705, 0.0000655737
+    fields, hist = _oracle_run(oracle, oracle.LDC, geo, 0.55, [1, 11, 21, max_it + 1])
     for k, steps in ((0, 1), (10, 11), (20, 21), (max_it + 1, max_it + 1)):
+        _, ux, uy, uz = fields[steps]
         got = (out / f"lid_{k}.vtk").read_text()
-        want = _oracle_vtk(gpu, oracle, geo, steps, str(tmp_path / f"o{k}.vtk"), oracle.LDC, C_U, CH, tau=0.55)
-        assert got == want, f"lid_{k}.vtk differs from the oracle's"
+        assert got == _vtk_ldc_independent(n, n, n, ux, uy, uz, C_U, CH), f"lid_{k}.vtk differs from the oracle's"
+    # residual k is the one after step k + 1 (ldc.cu:668); the loop ends after step max_it + 1
+    want = ["%g" % hist[k] for k in (0, 10, 20)]
+    assert [x.split("residual:")[1] for x in lines if x.startswith("ITERATION")] == want
+    assert log[:3] == want
+    assert lines[-1] == "Residual is %g" % hist[max_it]
+    assert log[-1].endswith(" ERROR IS%g" % hist[max_it])
 
 
 def test_poiseuille_driver(gpu, oracle, tmp_path):
     nx, ny, nz = 20, 24, 20
     out = tmp_path / "out"
-    subprocess.run([os.path.join(BIN, "poiseuille"), "--nx", str(nx), "--ny", str(ny), "--nz", str(nz),
-                    "--max-it", "12", "--time-save", "6", "--out", str(out)],
-                   capture_output=True, text=True, timeout=300, check=True)
+    r = subprocess.run([os.path.join(BIN, "poiseuille"), "--nx", str(nx), "--ny", str(ny), "--nz", str(nz),
+                        "--max-it", "12", "--time-save", "6", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300, check=True)
     geo = gpu.geo_poiseuille(nx, ny, nz)
-    files = sorted(os.listdir(out))
-    assert "CONVERGENCE.log" in files
-    got = (out / "pos_6.vtk").read_text()
-    want = _oracle_vtk(gpu, oracle, geo, 7, str(tmp_path / "o.vtk"), oracle.POISEUILLE, 1.5441, 0.0000655737,
-                       tau=0.58)
-    assert got == want
+    assert "CONVERGENCE.log" in os.listdir(out)
+    fields, hist = _oracle_run(oracle, oracle.POISEUILLE, geo, 0.58, [1, 7, 13])
+    for k, steps in ((0, 1), (6, 7), (12, 13)):
+        _, ux, uy, uz = fields[steps]
+        got = (out / f"pos_{k}.vtk").read_text()
+        assert got == _vtk_mask_independent(None, geo, ux, uy, uz, 1.5441, 0.0000655737), f"pos_{k}.vtk"
+    lines = r.stdout.strip().splitlines()
+    assert [x.split("residual:")[1] for x in lines if x.startswith("ITERATION")] == ["%g" % hist[k] for k in (0, 6, 12)]
 
 
 def _vtk_mask_independent(path_geo, geo, ux, uy, uz, C_U, CH):
