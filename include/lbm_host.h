@@ -37,7 +37,9 @@ typedef struct {
 /* geo_pre of a vessel mask: fluid = raw + 3 increments of the 6-neighbour minimum over the
  * interior (coronary.cu:58-73), the ends above, then ghost marking of the unused 18-neighbours
  * of every wall (coronary.cu:145-260).  Raster codes -1, 0, 1, 2, 3, 4 and 1 + passes. */
-void lbmh_geo_ends(int nx, int ny, int nz, const int32_t* raw, int n_ends, const lbmh_end* ends, int8_t* geo);
+int lbmh_geo_ends(int nx, int ny, int nz, const int32_t* raw, int n_ends, const lbmh_end* ends, int8_t* geo);
+/* ^ returns 0, or -1 (geo untouched) for a box under 3^3 or an end whose plane or window leaves
+ *   the interior (plane in [1, n-2], windows within [1, n-1)) or whose code 1 + passes > 127 */
 /* the reference's five ends for its NX x NY x NZ = 291 x 291 x 372 box (coronary.cu:75-143):
  * inlet x = 3 (one pass: code 2), main exit x = 272 (two: 3), sub-exits z = 185 (four: 5),
  * z = 191 (five: 6), z = 204 (six: 7).  Fills ends[5]; returns 5, or -1 when the box is too

@@ -145,8 +145,16 @@ long lbmh_read_geo_txt_zxy(const char* path, int nx, int ny, int nz, int32_t* ra
   return i;
 }
 
-void lbmh_geo_ends(int nx, int ny, int nz, const int32_t* raw, int n_ends, const lbmh_end* ends, int8_t* geo) {
+int lbmh_geo_ends(int nx, int ny, int nz, const int32_t* raw, int n_ends, const lbmh_end* ends, int8_t* geo) {
   const Box b{nx, ny, nz};
+  if (nx < 3 || ny < 3 || nz < 3 || n_ends < 0 || (n_ends > 0 && !ends)) return -1;
+  for (int e = 0; e < n_ends; ++e) {  // every cell of an end needs its four in-plane neighbours
+    const lbmh_end& E = ends[e];
+    const int n0 = E.axis == 0 ? ny : nx, n1 = E.axis == 0 ? nz : ny, np = E.axis == 0 ? nx : nz;
+    if ((E.axis != 0 && E.axis != 2) || E.plane < 1 || E.plane > np - 2 || E.lo0 < 1 || E.hi0 > n0 - 1 ||
+        E.lo1 < 1 || E.hi1 > n1 - 1 || E.passes < 0 || 1 + E.passes > 127)
+      return -1;
+  }
   std::vector<int> g(raw, raw + b.size());
   // fluid: three increments of the 6-neighbour minimum of the (unchanged) raw mask
   for (int z = 1; z < nz - 1; ++z)
@@ -171,6 +179,7 @@ void lbmh_geo_ends(int nx, int ny, int nz, const int32_t* raw, int n_ends, const
   }
   mark_ghosts(b, g, true);
   for (int64_t c = 0; c < b.size(); ++c) geo[c] = (int8_t)g[c];
+  return 0;
 }
 
 int lbmh_coronary_ends(int nx, int ny, int nz, lbmh_end* ends) {

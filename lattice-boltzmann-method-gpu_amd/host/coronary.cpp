@@ -47,12 +47,19 @@ int main(int argc, char** argv) {
   std::vector<lbmh_end> ends(5);
   if (args.has("--ends")) {
     ends = parse_ends(args.get("--ends", ""));
+    if (ends.empty()) {
+      std::fprintf(stderr, "--ends: no \"axis,plane,lo0,hi0,lo1,hi1,passes\" entries\n");
+      return 1;
+    }
   } else if (lbmh_coronary_ends(NX, NY, NZ, ends.data()) != 5) {
     std::fprintf(stderr, "a %dx%dx%d box cannot hold coronary.cu's end planes: give --ends\n", NX, NY, NZ);
     return 1;
   }
   std::vector<int8_t> geo(n);
-  lbmh_geo_ends(NX, NY, NZ, raw.data(), (int)ends.size(), ends.data(), geo.data());
+  if (lbmh_geo_ends(NX, NY, NZ, raw.data(), (int)ends.size(), ends.data(), geo.data()) != 0) {
+    std::fprintf(stderr, "invalid end table for a %dx%dx%d box\n", NX, NY, NZ);
+    return 1;
+  }
   raw.clear();
   raw.shrink_to_fit();
   const long NLATTICE = (long)lbmh_index_transform(NX, NY, NZ, geo.data(), nullptr);

@@ -137,7 +137,7 @@ def host_lib() -> C.CDLL:
             "lbmh_calc_res": (C.c_longdouble, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
             "lbmh_read_geo_txt_zxy": (C.c_long, [C.c_char_p, C.c_int, C.c_int, C.c_int, i32p]),
             "lbmh_calc_res_fluid": (C.c_longdouble, [C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p]),
-            "lbmh_geo_ends": (None, [C.c_int, C.c_int, C.c_int, i32p, C.c_int, C.POINTER(lbmh_end), i8p]),
+            "lbmh_geo_ends": (C.c_int, [C.c_int, C.c_int, C.c_int, i32p, C.c_int, C.POINTER(lbmh_end), i8p]),
             "lbmh_coronary_ends": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(lbmh_end)]),
             "lbmh_write_vtk_coronary": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, i8p, f32p, f32p, f32p, f32p,
                                                   C.c_float, C.c_float, C.c_float]),
@@ -281,7 +281,8 @@ def geo_ends(raw: np.ndarray, ends) -> np.ndarray:
     nz, ny, nx = raw.shape
     arr = (lbmh_end * max(1, len(ends)))(*[lbmh_end(*e) for e in ends])
     g = np.zeros(raw.shape, np.int8)
-    host_lib().lbmh_geo_ends(nx, ny, nz, _ptr(raw, C.c_int32), len(ends), arr, _ptr(g, C.c_int8))
+    if host_lib().lbmh_geo_ends(nx, ny, nz, _ptr(raw, C.c_int32), len(ends), arr, _ptr(g, C.c_int8)) != 0:
+        raise LbmError(f"lbmh_geo_ends: an end of {list(ends)} leaves the {nx}x{ny}x{nz} box's interior")
     return g
 
 

@@ -83,7 +83,9 @@ int main(int argc, char** argv) {
                               {2, 18, 1, nx - 1, 1, ny - 1, 4}};
     const int eo[21] = {0, 3, 1, ny - 1, 1, nz - 1, 1, 0, 25, 1, ny - 1, 1, nz - 1, 2, 2, 18, 1, nx - 1, 1, ny - 1, 4};
     std::vector<int8_t> g(n), go(n);
-    lbmh_geo_ends(nx, ny, nz, raw.data(), 3, ends, g.data());
+    if (lbmh_geo_ends(nx, ny, nz, raw.data(), 3, ends, g.data()) != 0) return fail("geo_ends status");
+    const lbmh_end bad = {0, 0, 1, ny - 1, 1, nz - 1, 1};  // plane on the box face: rejected
+    if (lbmh_geo_ends(nx, ny, nz, raw.data(), 1, &bad, go.data()) != -1) return fail("geo_ends bad end");
     orc_geo_coronary(nx, ny, nz, raw.data(), 3, eo, go.data());
     if (g != go) return fail("geo_ends");
     lbmh_end ref[5];

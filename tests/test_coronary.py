@@ -34,6 +34,16 @@ def test_geo_ends_small_vs_oracle(lbm, oracle):
     assert np.all(g[zz - 1, yy, xx] == 4)
 
 
+def test_geo_ends_rejects_ends_outside_the_interior(lbm):
+    from lbm_amd import cases
+    raw, ends = cases.coronary_small_vessel()
+    nz, ny, nx = raw.shape
+    for bad in [(0, 0, 1, ny - 1, 1, nz - 1, 1), (2, nz - 1, 1, nx - 1, 1, ny - 1, 1), (0, 3, 0, ny - 1, 1, nz - 1, 1),
+                (2, 30, 1, nx, 1, ny - 1, 4), (1, 5, 1, 5, 1, 5, 1)]:
+        with pytest.raises(lbm.LbmError):
+            lbm.geo_ends(raw, [bad])
+
+
 def test_geo_ends_reference_box_vs_oracle(lbm, oracle):
     from lbm_amd import cases
     raw = cases.coronary_reference_vessel()
