@@ -133,6 +133,16 @@ typedef struct {
   int row_axis;
 } lbm_desc;
 
+/* Checkpoint / resume (not in the reference, whose VTK output cannot restart a run; SURVEY.md
+ * section 5): the context's complete state -- both population buffers in the device layout, the
+ * NEE-adjacent cells' previous (rho, u), the step count and the convergence state -- to a file,
+ * and back into a context created with the same descriptor (extent, slab, case, tau and
+ * layout are checked; LBM_ERR_ARG otherwise).  A resumed run continues bit for bit.  Slab
+ * contexts save and load one file per rank (ghost planes included).
+ * A load that fails after the header checks (a truncated file) leaves the state unspecified. */
+int lbm_checkpoint_save(lbm_ctx* ctx, const char* path);
+int lbm_checkpoint_load(lbm_ctx* ctx, const char* path);
+
 /* Status / version */
 const char* lbm_version(void);
 const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error */

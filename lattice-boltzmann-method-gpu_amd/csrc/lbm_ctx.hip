@@ -1251,6 +1251,138 @@ int lbm_get_f(lbm_ctx* c, float* f) {
   return LBM_OK;
 }
 
+// ---- checkpoint / resume -------------------------------------------------------------------
+
+namespace {
+
+struct CkptHeader {
+  char magic[8];  // "LBMCKPT1"
+  int32_t version, nx, ny, nz, z_offset, nz_global, case_kind, swap, pitch, xshift, steps_done, cur;
+  int32_t last_slab;    // the last steps ran the slab ranges: their NEE lists hold the live (rho, u)
+  int32_t halo_primed;  // the ghost planes hold the exchange state (all 19 populations only at step 0)
+  uint32_t tau_bits;
+  int32_t nslow[3];  // whole, edge, mid NEE-adjacent lists
+  int64_t ncell, buf_floats;
+  ConvState conv;
+};
+
+constexpr size_t kCkptSlice = (size_t)64 << 20;  // bytes staged through the host per copy
+
+int ckpt_range_lists(lbm_ctx* c, Range* rs[3]) {
+  rs[0] = &c->whole;
+  rs[1] = &c->edge;
+  rs[2] = &c->mid;
+  return LBM_OK;
+}
+
+}  // namespace
+
+int lbm_checkpoint_save(lbm_ctx* c, const char* path) {
+  if (!c || !path) return LBM_ERR_ARG;
+  RCK(lbm_sync(c));
+  CkptHeader h{};
+  std::memcpy(h.magic, "LBMCKPT1", 8);
+  h.version = 1;
+  h.nx = c->L.nx; h.ny = c->L.ny; h.nz = c->L.nz;
+  h.z_offset = c->d.z_offset; h.nz_global = c->d.nz_global; h.case_kind = c->d.case_kind;
+  h.swap = c->L.swap; h.pitch = c->L.pitch; h.xshift = c->L.xshift;
+  h.steps_done = c->steps_done; h.cur = c->cur; h.last_slab = c->last_slab ? 1 : 0;
+  h.halo_primed = c->halo_primed ? 1 : 0;
+  std::memcpy(&h.tau_bits, &c->tau, 4);
+  Range* rs[3];
+  ckpt_range_lists(c, rs);
+  for (int i = 0; i < 3; ++i) h.nslow[i] = rs[i]->nslow;
+  h.ncell = c->L.ncell;
+  h.buf_floats = c->L.nchunk * kQ * kChunk;
+  HIPCK(c, hipMemcpy(&h.conv, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
+  std::FILE* f = std::fopen(path, "wb");
+  if (!f) {
+    c->err = std::string("lbm_checkpoint_save: cannot open ") + path;
+    return LBM_ERR_ARG;
+  }
+  bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
+  std::vector<char> stage(kCkptSlice);
+  auto dump = [&](const void* dev, size_t bytes) -> int {
+    for (size_t off = 0; ok && off < bytes; off += kCkptSlice) {
+      const size_t n = std::min(kCkptSlice, bytes - off);
+      HIPCK(c, hipMemcpy(stage.data(), static_cast<const char*>(dev) + off, n, hipMemcpyDeviceToHost));
+      ok = std::fwrite(stage.data(), 1, n, f) == n;
+    }
+    return LBM_OK;
+  };
+  int rc = LBM_OK;
+  // the current state and the buffer the last step read (the lazy macro read-out needs it)
+  for (int b : {c->cur, c->cur ^ 1})
+    if (rc == LBM_OK) rc = dump(c->buf[b], sizeof(float) * (size_t)h.buf_floats);
+  for (int i = 0; i < 3 && rc == LBM_OK; ++i)
+    if (rs[i]->nslow) rc = dump(rs[i]->prev, sizeof(float4) * (size_t)rs[i]->nslow);
+  if (std::fclose(f) != 0) ok = false;
+  if (rc != LBM_OK) return rc;
+  if (!ok) {
+    c->err = std::string("lbm_checkpoint_save: write failed: ") + path;
+    return LBM_ERR_ARG;
+  }
+  return LBM_OK;
+}
+
+int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
+  if (!c || !path) return LBM_ERR_ARG;
+  RCK(lbm_sync(c));
+  std::FILE* f = std::fopen(path, "rb");
+  if (!f) {
+    c->err = std::string("lbm_checkpoint_load: cannot open ") + path;
+    return LBM_ERR_ARG;
+  }
+  CkptHeader h{};
+  Range* rs[3];
+  ckpt_range_lists(c, rs);
+  uint32_t tau_bits;
+  std::memcpy(&tau_bits, &c->tau, 4);
+  bool match = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, "LBMCKPT1", 8) == 0 && h.version == 1 &&
+               h.nx == c->L.nx && h.ny == c->L.ny && h.nz == c->L.nz && h.z_offset == c->d.z_offset &&
+               h.nz_global == c->d.nz_global && h.case_kind == c->d.case_kind && h.swap == c->L.swap &&
+               h.pitch == c->L.pitch && h.xshift == c->L.xshift && h.tau_bits == tau_bits &&
+               h.ncell == c->L.ncell && h.buf_floats == c->L.nchunk * kQ * kChunk;
+  for (int i = 0; i < 3 && match; ++i) match = h.nslow[i] == rs[i]->nslow;
+  if (!match) {
+    std::fclose(f);
+    c->err = std::string("lbm_checkpoint_load: ") + path +
+             " is not a checkpoint of a lattice with this descriptor (extent, slab, case, tau, layout)";
+    return LBM_ERR_ARG;
+  }
+  std::vector<char> stage(kCkptSlice);
+  bool ok = true;
+  auto fill = [&](void* dev, size_t bytes) -> int {
+    for (size_t off = 0; ok && off < bytes; off += kCkptSlice) {
+      const size_t n = std::min(kCkptSlice, bytes - off);
+      ok = std::fread(stage.data(), 1, n, f) == n;
+      if (ok) HIPCK(c, hipMemcpy(static_cast<char*>(dev) + off, stage.data(), n, hipMemcpyHostToDevice));
+    }
+    return LBM_OK;
+  };
+  int rc = LBM_OK;
+  for (int b : {h.cur, h.cur ^ 1})
+    if (rc == LBM_OK) rc = fill(c->buf[b], sizeof(float) * (size_t)h.buf_floats);
+  for (int i = 0; i < 3 && rc == LBM_OK; ++i)
+    if (rs[i]->nslow) rc = fill(rs[i]->prev, sizeof(float4) * (size_t)rs[i]->nslow);
+  std::fclose(f);
+  if (rc != LBM_OK) return rc;
+  if (!ok) {
+    c->err = std::string("lbm_checkpoint_load: truncated file ") + path;
+    return LBM_ERR_ARG;
+  }
+  HIPCK(c, hipMemcpy(c->conv, &h.conv, sizeof(ConvState), hipMemcpyHostToDevice));
+  c->cur = h.cur;
+  c->steps_done = h.steps_done;
+  c->macros_stale = h.steps_done > 0;
+  c->last_slab = h.last_slab != 0;
+  // the saved ghost planes are the exchange's own state: after the first step only the 5
+  // crossing populations are exchanged, and a ghost wall's other slots hold this slab's
+  // bounce-back values, which a fresh 19-population exchange would overwrite
+  c->halo_primed = h.halo_primed != 0;
+  return LBM_OK;
+}
+
 int lbm_get_counts(lbm_ctx* c, int64_t* n_box, int64_t* n_fluid, double* algo_bytes_per_step) {
   if (!c) return LBM_ERR_ARG;
   if (n_box) *n_box = c->n_box;

@@ -85,7 +85,7 @@ LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_tune", "lbm_get_nonfinite", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
-    "lbm_get_layout", "lbm_buffer_placement",
+    "lbm_get_layout", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream",
 ]
 HOST_SYMBOLS = [
@@ -179,6 +179,8 @@ def lbm_lib() -> C.CDLL:
             "lbm_stats": (C.c_int, [P, f64p, i64p, f64p]),
             "lbm_kernel_times": (C.c_int, [P, C.c_int, f64p, i64p]),
             "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
+            "lbm_checkpoint_save": (C.c_int, [P, C.c_char_p]),
+            "lbm_checkpoint_load": (C.c_int, [P, C.c_char_p]),
             "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
             "lbm_get_layout": (C.c_int, [P, ip, ip, ip, i64p]),
             "lbm_buffer_placement": (C.c_int, [P, f64p, C.c_int, ip, ip]),
@@ -511,6 +513,14 @@ class Lattice:
         a = np.zeros((19,) + self.shape, np.float32)
         self._ck(lbm_lib().lbm_get_f(self.h, _ptr(a, C.c_float)), "lbm_get_f")
         return a
+
+    def checkpoint_save(self, path: str) -> None:
+        """The complete lattice state to a file (lbm_checkpoint_save)."""
+        self._ck(lbm_lib().lbm_checkpoint_save(self.h, os.fsencode(path)), "lbm_checkpoint_save")
+
+    def checkpoint_load(self, path: str) -> None:
+        """Resume from lbm_checkpoint_save's file (same descriptor; lbm_checkpoint_load)."""
+        self._ck(lbm_lib().lbm_checkpoint_load(self.h, os.fsencode(path)), "lbm_checkpoint_load")
 
     def counts(self):
         nb, nf, by = C.c_int64(), C.c_int64(), C.c_double()

@@ -1,0 +1,159 @@
+"""Checkpoint / resume (lbm_checkpoint_save / lbm_checkpoint_load; SURVEY.md section 5: the
+reference cannot restart a run).  A run saved after k steps and resumed in a fresh context
+continues bit for bit: populations, macros (the lazy read-out right after the load included),
+the residual history and the convergence state -- on every boundary kind whose state is more
+than the populations (the NEE-adjacent cells' previous (rho, u)), on both step paths, and for
+z-slabs stepped together."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b, what):
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), what
+
+
+def _builders():
+    from lbm_amd import cases
+    raw, ends = cases.coronary_small_vessel()
+    return {
+        "ldc": lambda: cases.ldc(24)[0],
+        "poiseuille": lambda: cases.poiseuille(20, 28, 20)[0],
+        "bifurcation": lambda: cases.bifurcation(1)[0],
+        "coronary": lambda: cases.coronary(raw, ends)[0],
+    }
+
+
+@pytest.mark.parametrize("case", ["ldc", "poiseuille", "bifurcation", "coronary"])
+def test_resume_is_bitwise(gpu, tmp_path, cells_per_lane, case):
+    make = _builders()[case]
+    a = make()
+    a.step(7)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    ha = a.step(25)
+    b = make()
+    b.checkpoint_load(path)
+    hb = b.step(25)
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32)), f"{case}: residual histories differ"
+    _same(a.macros(), b.macros(), f"{case}: macros differ after resuming")
+    assert np.array_equal(a.f().view(np.uint32), b.f().view(np.uint32)), f"{case}: populations differ"
+    assert a.state()["k"] == b.state()["k"] == 32
+    a.close()
+    b.close()
+
+
+def test_resume_macros_right_after_load(gpu, tmp_path):
+    from lbm_amd import cases
+    a, geo, _, _ = cases.bifurcation(1)
+    a.step(11)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    b, _, _, _ = cases.bifurcation(1)
+    b.checkpoint_load(path)
+    _same(a.macros(), b.macros(), "lazy macro read-out after a load")
+    a.close()
+    b.close()
+
+
+def test_resume_under_convergence_control(gpu, tmp_path):
+    """Saved mid-run with the stopping rule on: the resumed run stops at the same step."""
+    from lbm_amd import cases
+    a = cases.ldc(16)[0]
+    a.set_convergence(True, 10000, 50, 1e-6)
+    a.step(300, history=False)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    a.step(10001, history=False)
+    sa = a.state()
+    b = cases.ldc(16)[0]
+    b.set_convergence(True, 10000, 50, 1e-6)
+    b.checkpoint_load(path)
+    b.step(10001, history=False)
+    sb = b.state()
+    assert sa["stopped"] == sb["stopped"] == 1 and sa["k"] == sb["k"] and sa["residual"] == sb["residual"]
+    _same(a.macros(), b.macros(), "converged fields")
+    a.close()
+    b.close()
+
+
+def test_resume_slabs(gpu, tmp_path):
+    """Three z-slabs stepped together (lbm_group_step), one file per slab."""
+    from lbm_amd import cases, initial_fields, Lattice, LBM_CASE_POISEUILLE, LBM_INIT_EXPANDED
+    import lbm_amd
+    nx, ny, nz = 24, 30, 33
+    _, geo = cases.poiseuille(nx, ny, nz)
+    prof = lbm_amd.poiseuille_profile(nx, nz)
+    rho, ux, uy, uz = initial_fields(1, geo)
+    xa = lbm_amd.x_align_for(geo, LBM_CASE_POISEUILLE)
+
+    def slabs():
+        out = []
+        for i in range(3):
+            z0, z1 = cases.slab_bounds(nz, 3, i)
+            lat = Lattice(LBM_CASE_POISEUILLE, (z1 - z0, ny, nx), 0.58, cases.slab_geo(geo, z0, z1),
+                          halo_planes=True, inlet_uy=prof, outlet_uy=prof, z_offset=z0, nz_global=nz, x_align=xa)
+            lat.init_equilibrium(LBM_INIT_EXPANDED, rho[z0:z1], ux[z0:z1], uy[z0:z1], uz[z0:z1])
+            out.append(lat)
+        return out
+
+    a = slabs()
+    lbm_amd.group_step(a, 9)
+    for i, lat in enumerate(a):
+        lat.checkpoint_save(str(tmp_path / f"ck{i}.bin"))
+    ha = lbm_amd.group_step(a, 30)
+    b = slabs()
+    for i, lat in enumerate(b):
+        lat.checkpoint_load(str(tmp_path / f"ck{i}.bin"))
+    hb = lbm_amd.group_step(b, 30)
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32))
+    for x, y in zip(a, b):
+        _same(x.macros(), y.macros(), "slab macros")
+        x.close()
+        y.close()
+
+
+def test_load_rejects_other_lattices(gpu, tmp_path):
+    from lbm_amd import cases
+    import lbm_amd
+    a = cases.ldc(24)[0]
+    a.step(3)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    for other in (cases.ldc(20)[0], cases.ldc(24, tau=0.6)[0], cases.poiseuille(24, 24, 24)[0]):
+        with pytest.raises(lbm_amd.LbmError):
+            other.checkpoint_load(path)
+        other.close()
+    (tmp_path / "short.bin").write_bytes(open(path, "rb").read()[:4096])
+    with pytest.raises(lbm_amd.LbmError):
+        a.checkpoint_load(str(tmp_path / "short.bin"))
+    with pytest.raises(lbm_amd.LbmError):
+        a.checkpoint_load(str(tmp_path / "missing.bin"))
+    a.close()
+
+
+def test_resume_rccl_slab(gpu, tmp_path):
+    """A slab context on a one-rank RCCL communicator (the multi-GPU step sequence: edge and
+    interior launches, parity-slot reduction, all-reduce, finisher) saved and resumed."""
+    from lbm_amd import cases
+    import lbm_amd
+
+    def make():
+        lat = cases.ldc_device(32, 32, 32, z_offset=32, nz_global=96)
+        lat.attach_rccl(lbm_amd.rccl_unique_id(), 0, 1)
+        return lat
+
+    a = make()
+    a.step(6)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    ha = a.step(20)
+    b = make()
+    b.checkpoint_load(path)
+    hb = b.step(20)
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32))
+    _same(a.macros(), b.macros(), "RCCL slab macros")
+    a.close()
+    b.close()
