@@ -13,6 +13,7 @@
 // RCCL on a second stream while the interior updates.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1132,6 +1133,11 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
     return LBM_OK;
   }
   HIPCK(c, hipSetDevice(c->d.device));
+  // a roctx range per call (rocprofv3 --marker-trace): the host side of the step loop
+  struct Range_ {
+    Range_() { roctxRangePush("lbm_step"); }
+    ~Range_() { roctxRangePop(); }
+  } roctx_range;
   const bool want_hist = residual_hist != nullptr;
   const int k0 = c->steps_done, cur0 = c->cur;
   if (want_hist) {
