@@ -149,7 +149,7 @@ const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error
 
 /* Process-wide tuning knobs (not a reference interface: A/B measurement and test switches;
  * the defaults are the measured best).  Read when a context is created (ROW_AXIS,
- * CELLS_PER_LANE, EXACT_DIV, FUSED_RESIDUAL, BUFFER_ALLOC, PERSISTENT).  Returns the previous value, or
+ * CELLS_PER_LANE, EXACT_DIV, FUSED_RESIDUAL, BUFFER_ALLOC).  Returns the previous value, or
  * LBM_ERR_ARG for an unknown knob / value.  Results are bit-identical for every setting. */
 typedef enum {
   LBM_TUNE_ROW_AXIS = 0,        /* stands in for lbm_desc.row_axis = 0: 0 choose, 1 x, 2 y */
@@ -162,10 +162,7 @@ typedef enum {
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
                                    asynchronous RCCL error always aborts promptly. */
-  LBM_TUNE_PERSISTENT = 6,      /* small single-domain lattices (<= 4 active chunks per CU, one
-                                   cell per lane): 0 (default) one persistent launch per lbm_step
-                                   call (k_persist), 1 one k_step1 launch per step */
-  LBM_TUNE_COUNT = 7
+  LBM_TUNE_COUNT = 6
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 
@@ -257,10 +254,6 @@ int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen
  * 2 = y; pitch = row slots; x_align 1..4; active_chunks = 256-cell chunks k_step launches a
  * wave for (those holding fluid).  Nullable outputs. */
 int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_t* active_chunks);
-/* Which step path lbm_step takes on a single domain: 4 = four cells per lane (k_step), 1 = one
- * cell per lane with one k_step1 launch per step, 2 = one persistent k_persist launch per
- * lbm_step call (small lattices, LBM_TUNE_PERSISTENT); workgroups: k_persist's grid (else 0). */
-int lbm_get_step_path(lbm_ctx* ctx, int* path, int* workgroups);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (done by the NEE blocks of
  * the step kernel). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);

@@ -34,7 +34,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -119,19 +119,6 @@ struct lbm_ctx {
   // from the last step's source buffer when macros_stale
   bool macros_stale = false;
   bool last_slab = false;  // the last steps ran the slab ranges (edge + mid), not whole
-  // persistent multi-step path (k_persist, lbm_kernels.hpp): small single-domain lattices
-  struct Persist {
-    bool on = false;
-    int G = 0, m = 0;            // workgroups (one per CU at most), chunks per workgroup
-    int2* deps = nullptr;        // per workgroup: first / last workgroup its pulls reach
-    int* nee_of = nullptr;       // per cell: index in whole's NEE-adjacent list, or -1
-    float4* prev1 = nullptr;     // second (rho, u) array of the NEE-adjacent cells (odd steps)
-    int* ctl = nullptr;          // kCtl* words + G step flags (zeroed per launch)
-    double* part = nullptr;      // 4 x G step partials
-    float* z = nullptr;          // third population allocation (rotation under convergence control)
-    bool unchecked = false;      // launched since the last abort check
-    bool rotated = false;        // the last call rotated through {alloc[cur], alloc[cur ^ 1], z}
-  } pm;
   // rccl
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -463,78 +450,6 @@ void free_range(Range& r) {
   r = Range{};
 }
 
-// The persistent path (k_persist) for the whole range when it is small: one cell per lane,
-// the fewest chunks per workgroup (1, 2 or 4) for which the step workgroups plus the reducer
-// fit the device at the occupancy query's blocks per CU (at most 4: independent workgroups
-// sharing a CU overlap one's VALU with another's memory waits), and every workgroup's pulls
-// reach at most 61 workgroups (one poll instruction).  Otherwise one k_step1 launch per step.
-int setup_persist(lbm_ctx* c) {
-  Range& r = c->whole;
-  if (g_tune[LBM_TUNE_PERSISTENT] == 1 || !r.quarter || r.nchunks == 0) return LBM_OK;
-  if ((double)c->L.buf_floats() * sizeof(float) >= 2147483648.0 || c->L.ncell >= (int64_t(1) << 30)) return LBM_OK;
-  hipDeviceProp_t prop;
-  HIPCK(c, hipGetDeviceProperties(&prop, c->d.device));
-  const int cus = prop.multiProcessorCount;
-  std::vector<int> ids(r.nchunks);
-  if (r.chunk0 >= 0) {
-    for (int i = 0; i < r.nchunks; ++i) ids[i] = r.chunk0 + i;
-  } else {
-    HIPCK(c, hipMemcpy(ids.data(), r.chunks, sizeof(int) * r.nchunks, hipMemcpyDeviceToHost));
-  }
-  // a cell pulls from at most plane + pitch + 1 cells away: chunks within D of its own
-  const int64_t D = (c->L.plane + c->L.pitch + 1) / kChunk + 2;
-  std::vector<int2> deps;
-  int m = 0, G = 0;
-  const int mmin = g_tune[LBM_TUNE_PERSISTENT] >= 2 ? 1 << (g_tune[LBM_TUNE_PERSISTENT] - 1) : 1;  // lab: 2 -> m >= 2, 3 -> m = 4
-  for (int mm : {1, 2, 4}) {
-    if (mm < mmin) continue;
-    const int bpc = std::min(4, persist_blocks_per_cu(mm, c->L.swap));
-    const int g = (r.nchunks + mm - 1) / mm;
-    if (bpc < 1 || g + 1 > cus * bpc) continue;
-    std::vector<int2> dv(g);
-    bool ok = true;
-    for (int w = 0; w < g && ok; ++w) {
-      const int64_t lo = ids[w * mm] - D, hi = ids[std::min((w + 1) * mm, r.nchunks) - 1] + D;
-      const int plo = (int)(std::lower_bound(ids.begin(), ids.end(), lo) - ids.begin());
-      const int phi = (int)(std::upper_bound(ids.begin(), ids.end(), hi) - ids.begin()) - 1;
-      dv[w] = make_int2(plo / mm, phi / mm);
-      ok = dv[w].y - dv[w].x + 1 <= 61;
-    }
-    if (!ok) continue;
-    m = mm;
-    G = g;
-    deps.swap(dv);
-    break;
-  }
-  if (!m) return LBM_OK;
-  HIPCK(c, hipMalloc(&c->pm.deps, sizeof(int2) * G));
-  HIPCK(c, hipMemcpy(c->pm.deps, deps.data(), sizeof(int2) * G, hipMemcpyHostToDevice));
-  std::vector<int> nee_of((size_t)c->L.ncell, -1);
-  if (r.nslow) {
-    std::vector<int> cells(r.nslow);
-    HIPCK(c, hipMemcpy(cells.data(), r.cells, sizeof(int) * r.nslow, hipMemcpyDeviceToHost));
-    for (int i = 0; i < r.nslow; ++i) nee_of[cells[i]] = i;
-    HIPCK(c, hipMalloc(&c->pm.prev1, sizeof(float4) * r.nslow));
-  }
-  HIPCK(c, hipMalloc(&c->pm.nee_of, sizeof(int) * c->L.ncell));
-  HIPCK(c, hipMemcpy(c->pm.nee_of, nee_of.data(), sizeof(int) * c->L.ncell, hipMemcpyHostToDevice));
-  HIPCK(c, hipMalloc(&c->pm.ctl, sizeof(int) * (kCtlFlags + G)));
-  HIPCK(c, hipMemset(c->pm.ctl, 0, sizeof(int) * (kCtlFlags + G)));
-  HIPCK(c, hipMalloc(&c->pm.part, sizeof(double) * 4 * G));
-  HIPCK(c, hipMalloc(&c->pm.z, sizeof(float) * c->L.buf_floats()));
-  c->pm.G = G;
-  c->pm.m = m;
-  c->pm.on = true;
-  return LBM_OK;
-}
-
-void free_persist(lbm_ctx* c) {
-  for (void* p : {(void*)c->pm.deps, (void*)c->pm.nee_of, (void*)c->pm.prev1, (void*)c->pm.ctl, (void*)c->pm.part,
-                  (void*)c->pm.z})
-    if (p) (void)hipFree(p);
-  c->pm = lbm_ctx::Persist{};
-}
-
 int ensure_hist(lbm_ctx* c, int n) {
   if (n <= c->hist_cap) return LBM_OK;
   if (c->hist) HIPCK(c, hipFree(c->hist));
@@ -649,7 +564,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 3};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -890,7 +805,6 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     }
     c->edge.part = c->whole.part + c->whole.npart;
     c->mid.part = c->edge.part + c->edge.npart;
-    if (setup_persist(c) != LBM_OK) return bail(LBM_ERR_HIP);
   }
 #undef CK
   *out = c;
@@ -907,7 +821,6 @@ void lbm_destroy(lbm_ctx* c) {
                    c->recv_up, c->recv_dn})
     if (p) (void)hipFree(p);
   for (Range* r : {&c->whole, &c->edge, &c->mid}) free_range(*r);
-  free_persist(c);
   if (c->type) (void)hipFree(c->type);
   if (c->links) (void)hipFree(c->links);
   if (c->codes) (void)hipFree(c->codes);
@@ -1094,82 +1007,7 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
   return LBM_OK;
 }
 
-// every step of the call in one k_persist launch (lbm_ctx::pm)
-int step_persist(lbm_ctx* c, int nsteps, bool want_hist) {
-  const Range& r = c->whole;
-  const lbm_ctx::Persist& pm = c->pm;
-  PersistArgs p{};
-  const size_t bytes = sizeof(float) * c->L.buf_floats();
-  if (c->conv_enabled) {
-    // three buffers in rotation: the step a launch may run past the stop step lands in the
-    // third one, so the stop step's source (the macro read-out's input) survives.  z takes the
-    // static content (pulled passive cells, guards) from the current state; lbm_step re-labels
-    // the three allocations from the device's step count after the call.
-    p.buf0 = c->alloc[c->cur];
-    p.buf1 = c->alloc[c->cur ^ 1];
-    p.buf2 = c->pm.z;
-    p.rot3 = 1;
-    HIPCK(c, hipMemcpyAsync(c->pm.z, c->alloc[c->cur], bytes, hipMemcpyDeviceToDevice, c->s_comp));
-    c->pm.rotated = true;
-  } else {
-    p.buf0 = c->alloc[0];
-    p.buf1 = c->alloc[1];
-    p.buf2 = c->pm.z;
-    p.rot3 = 0;
-  }
-  p.buf_bytes = (uint32_t)(sizeof(float) * c->L.buf_floats());
-  p.gfl = (int)(c->L.guard * kQ * kChunk);
-  p.cur0 = c->cur;
-  p.type = c->type; p.links = c->links; p.nee_of = pm.nee_of;
-  p.rho = c->rho; p.ux = c->ux; p.uy = c->uy; p.uz = c->uz;
-  p.prev0 = r.prev; p.prev1 = pm.prev1;
-  p.prev_bytes = (uint32_t)(sizeof(float4) * std::max(1, r.nslow));
-  p.nee_mask = r.nee_mask; p.nee_bc = r.nee_bc;
-  p.chunks = r.chunks; p.chunk0 = r.chunk0; p.nchunks = r.nchunks;
-  p.pitch = c->L.pitch; p.plane = (int)c->L.plane;
-  p.c_lo = (int)r.c_lo; p.c_hi = (int)r.c_hi;
-  p.tau = c->tau; p.tau_rcp = 1.0f / c->tau; p.omc = c->omc;
-  p.tau_fast = c->fast_div ? 1 : 0;
-  p.h0 = c->steps_done;
-  p.nsteps = nsteps;
-  p.G = pm.G; p.m = pm.m;
-  p.deps = pm.deps;
-  p.cv = c->conv;
-  p.hist = want_hist ? c->hist : nullptr;
-  p.ctl = pm.ctl;
-  p.part = pm.part;
-  p.timeout_ticks = 200000000ull;  // 2 s at 100 MHz: no wait of a resident grid comes near it
-  p.swap = c->L.swap;
-  HIPCK(c, hipMemsetAsync(pm.ctl, 0, sizeof(int) * (kCtlFlags + pm.G), c->s_comp));
-  c->launches++;
-  RCK(timed(c, c->s_comp, kKindStep, kKindSrc0 + c->cur, -1, [&] {
-    HIPCK(c, launch_persist(p, c->s_comp));
-    return LBM_OK;
-  }));
-  HIPCK(c, launch_prev_fix(r.prev, pm.prev1, r.nslow, c->conv, pm.ctl, c->s_comp));
-  c->pm.unchecked = true;
-  if (nsteps & 1) c->cur ^= 1;  // convergence control: lbm_step re-labels from the device's k
-  return LBM_OK;
-}
-
-// after a rotating k_persist call that ran K steps: state K in ring[K % 3], its source in
-// ring[(K - 1) % 3] (ring = alloc[cur], alloc[cur ^ 1], z at the call's start)
-void persist_relabel(lbm_ctx* c, int cur0, int K) {
-  c->pm.rotated = false;
-  if (K <= 0) {
-    c->cur = cur0;
-    return;
-  }
-  float* ring[3] = {c->alloc[cur0], c->alloc[cur0 ^ 1], c->pm.z};
-  c->alloc[0] = ring[K % 3];
-  c->alloc[1] = ring[(K + 2) % 3];
-  c->pm.z = ring[(K + 1) % 3];
-  c->cur = 0;
-  for (int b = 0; b < 2; ++b) c->buf[b] = c->alloc[b] + c->L.guard * kQ * kChunk;
-}
-
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
-  if (c->pm.on) return step_persist(c, nsteps, want_hist);
   int h = c->steps_done;
   if (c->fuse_red && !c->conv_enabled) {
     // one launch per step: step s's k_step also finishes step s-1's residual; the last
@@ -1237,15 +1075,6 @@ int wait_streams(lbm_ctx* c) {
   if (!c->comm) {
     HIPCK(c, hipStreamSynchronize(c->s_comp));
     HIPCK(c, hipStreamSynchronize(c->s_comm));
-    if (c->pm.unchecked) {  // a k_persist wait that timed out leaves the lattice undefined
-      int ab = 0;
-      HIPCK(c, hipMemcpy(&ab, c->pm.ctl + kCtlAbort, sizeof(int), hipMemcpyDeviceToHost));
-      c->pm.unchecked = false;
-      if (ab) {
-        c->err = "persistent step kernel: a workgroup wait timed out (grid not co-resident?)";
-        return LBM_ERR_HIP;
-      }
-    }
     return LBM_OK;
   }
   const auto t0 = std::chrono::steady_clock::now();
@@ -1324,8 +1153,7 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
     ConvState h{};
     HIPCK(c, hipMemcpy(&h, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
     c->steps_done = h.k;  // device-confirmed (a converged run stops early)
-    if (c->pm.rotated) persist_relabel(c, cur0, h.k - k0);
-    else if (c->conv_enabled) c->cur = cur0 ^ ((h.k - k0) & 1);  // one step per launch under convergence control
+    if (c->conv_enabled) c->cur = cur0 ^ ((h.k - k0) & 1);  // one step per launch under convergence control
     if (want_hist) HIPCK(c, hipMemcpy(residual_hist, c->hist, sizeof(float) * nsteps, hipMemcpyDeviceToHost));
     if (steps_done) *steps_done = c->steps_done;
   } else {
@@ -1566,13 +1394,6 @@ int lbm_get_counts(lbm_ctx* c, int64_t* n_box, int64_t* n_fluid, double* algo_by
   if (n_box) *n_box = c->n_box;
   if (n_fluid) *n_fluid = c->n_fluid;
   if (algo_bytes_per_step) *algo_bytes_per_step = 152.0 * (double)c->n_fluid;
-  return LBM_OK;
-}
-
-int lbm_get_step_path(lbm_ctx* c, int* path, int* workgroups) {
-  if (!c) return LBM_ERR_ARG;
-  if (path) *path = c->pm.on ? 2 : c->whole.quarter ? 1 : 4;
-  if (workgroups) *workgroups = c->pm.on ? c->pm.G : 0;
   return LBM_OK;
 }
 

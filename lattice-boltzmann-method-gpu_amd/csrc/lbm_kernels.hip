@@ -1044,308 +1044,6 @@ __global__ void k_digest(const uint8_t* __restrict__ type, const float* __restri
   if (threadIdx.x == 0) atomicAdd(out + zl, part[0] + part[1] + part[2] + part[3]);
 }
 
-// ---- persistent multi-step kernel (small lattices; lbm_kernels.hpp, PersistArgs) ----------
-// At 64^3 a step of k_step1 is ~13 us, of which the kernel boundary, the grid's fill and drain
-// and the residual tail are a third: one launch per lbm_step call keeps every workgroup
-// resident and replaces the grid-wide step boundary by waits on the few workgroups whose
-// populations a workgroup pulls.  Cell arithmetic is process_cell1 / nee_cell's, bit for bit.
-
-constexpr int kSc1 = 16;  // buffer cache policy sc1: loads bypass L1 (L2-served), stores write through
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ float co_ld(__amdgpu_buffer_rsrc_t r, uint32_t i) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, i * 4u, 0, kSc1));
-}
-__device__ __forceinline__ void co_st(__amdgpu_buffer_rsrc_t r, uint32_t i, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, i * 4u, 0, kSc1);
-}
-__device__ __forceinline__ int ld_agent(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// population q of cell c, in floats from the allocation's base (32-bit: guard chunks keep
-// c - e_q's chunk >= -guard, so the sum stays positive)
-__device__ __forceinline__ uint32_t pidx(int c, int q, int gfl) {
-  return (uint32_t)(((c >> 8) * kQ + q) * kChunk + (c & (kChunk - 1)) + gfl);
-}
-
-template <bool SW, int... Qs>
-__device__ __forceinline__ void co_pull_all(float* f, __amdgpu_buffer_rsrc_t rs, int c, int gfl, int pitch, int plane,
-                                            std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = co_ld(rs, pidx(c - (int)cell_off<Qs, SW>(pitch, plane), Qs, gfl))), ...);
-}
-template <int Q, bool SW>
-__device__ __forceinline__ void co_bb_one(__amdgpu_buffer_rsrc_t rd, int c, uint32_t m, float out_opp, int gfl,
-                                          int pitch, int plane) {
-  if constexpr (Q > 0) {
-    if (m & (1u << Q)) co_st(rd, pidx(c - (int)cell_off<Q, SW>(pitch, plane), Q, gfl), out_opp);
-  }
-}
-template <bool SW, int... Qs>
-__device__ __forceinline__ void co_store_all(const float* f, __amdgpu_buffer_rsrc_t rd, int c, uint32_t m, int gfl,
-                                             int pitch, int plane, std::integer_sequence<int, Qs...>) {
-  (co_st(rd, pidx(c, Qs, gfl), f[Qs]), ...);
-  if (m) (co_bb_one<Qs, SW>(rd, c, m, f[Dir<Qs>::opp], gfl, pitch, plane), ...);
-}
-
-// nee_put / nee_pull_all's substitution with sc1 loads of the cell's own slots
-template <int Q, bool SW>
-__device__ __forceinline__ void co_nee_put(float* f, const float* nv, const PersistArgs& p, __amdgpu_buffer_rsrc_t rs,
-                                           int c, const Macro& mp, uint32_t nee, uint32_t press) {
-  if constexpr (Q > 0) {
-    if (nee & (1u << Q)) {
-      const int k = __builtin_popcount(nee & ((1u << Q) - 1u));
-      float v = nv[0];
-#pragma unroll
-      for (int j = 1; j < kNeeSlots; ++j)
-        if (k == j) v = nv[j];
-      if (k >= kNeeSlots) {  // beyond the slots (edges/corners of several faces)
-        const int nb = c - (int)cell_off<Q, SW>(p.pitch, p.plane);
-        v = nee_value<Q>(NeeSlot{co_ld(rs, pidx(c, Q, p.gfl)), p.rho[nb], p.ux[nb], p.uy[nb], p.uz[nb]}, mp,
-                         (press >> Q) & 1u, p.omc);
-      }
-      f[Q] = v;
-    }
-  }
-}
-template <bool SW, int... Qs>
-__device__ __forceinline__ void co_nee_apply(float* f, const PersistArgs& p, __amdgpu_buffer_rsrc_t rs, int c,
-                                             const Macro& mp, uint2 m, const float4* bc,
-                                             std::integer_sequence<int, Qs...>) {
-  const uint32_t nee = m.x;
-  NeeSlot sl[kNeeSlots];
-  int qs[kNeeSlots];
-  uint32_t rest = nee;
-#pragma unroll
-  for (int j = 0; j < kNeeSlots; ++j) {
-    qs[j] = 0;
-    if (rest) {
-      const int q = __builtin_ctz(rest);
-      rest &= rest - 1u;
-      qs[j] = q;
-      sl[j] = nee_slot(co_ld(rs, pidx(c, q, p.gfl)), bc[j]);
-    }
-  }
-  float nv[kNeeSlots];
-#pragma unroll
-  for (int j = 0; j < kNeeSlots; ++j)
-    nv[j] = qs[j] ? nee_value_rt(qs[j], sl[j], mp, (m.y >> qs[j]) & 1u, p.omc) : 0.f;
-  (co_nee_put<Qs, SW>(f, nv, p, rs, c, mp, nee, m.y), ...);
-}
-
-// one cell: process_cell1 for a fluid cell, nee_cell for an NEE-adjacent one (its previous
-// (rho, u) from rp_in, the new ones to rp_out)
-template <bool SW>
-__device__ __forceinline__ double co_cell(const PersistArgs& p, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd,
-                                          __amdgpu_buffer_rsrc_t rp_in, __amdgpu_buffer_rsrc_t rp_out, int c,
-                                          bool nee_active) {
-  const uint8_t t = p.type[c];
-  const uint32_t links = p.links[c];
-  const int ni = p.nee_of[c];
-  float f[kQ];
-  co_pull_all<SW>(f, rs, c, p.gfl, p.pitch, p.plane, AllQ{});
-  if (!(c >= p.c_lo && c < p.c_hi && (t & kClassMask) == kFluid)) return 0.0;
-  const bool nee_adj = (t & kNeedsMac) != 0;
-  if (nee_adj) {
-    const Macro mp{co_ld(rp_in, 4 * ni), co_ld(rp_in, 4 * ni + 1), co_ld(rp_in, 4 * ni + 2), co_ld(rp_in, 4 * ni + 3)};
-    const uint2 mk = p.nee_mask[ni];
-    float4 bc[kNeeSlots];
-#pragma unroll
-    for (int j = 0; j < kNeeSlots; ++j) bc[j] = p.nee_bc[ni * kNeeSlots + j];
-    if (nee_active && mk.x) co_nee_apply<SW>(f, p, rs, c, mp, mk, bc, AllQ{});
-  }
-  float rho = 0.f;
-#pragma unroll
-  for (int q = 0; q < kQ; ++q) rho = rho + f[q];
-  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
-  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
-  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  const bool ok = fast_div_ok1(f, ux, uy, uz);
-  if (p.tau_fast && __all(ok)) fix_relax_fast_all(f, p.tau, p.tau_rcp, rho, ux, uy, uz, AllQ{});
-  else fix_relax_all(f, p.tau, rho, ux, uy, uz, AllQ{});
-  co_store_all<SW>(f, rd, c, links, p.gfl, p.pitch, p.plane, AllQ{});
-  if (nee_adj) {
-    co_st(rp_out, 4 * ni, rho);
-    co_st(rp_out, 4 * ni + 1, ux);
-    co_st(rp_out, 4 * ni + 2, uy);
-    co_st(rp_out, 4 * ni + 3, uz);
-  }
-  return (double)sqrtf(ux * ux + uy * uy + uz * uz);
-}
-
-// spin (one lane) until *w >= v; false on abort or after timeout ticks (then raises abort)
-__device__ bool co_wait_geq(const int* w, int v, int* ctl, uint64_t timeout) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (ld_agent(w) >= v) return true;
-    if (ld_agent(ctl + kCtlAbort)) return false;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-      st_agent(ctl + kCtlAbort, 1);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// residual_logic on the device-resident state with sc1 loads and stores; returns stopped
-__device__ int co_residual(ConvState* cv, double S, float* hist_slot) {
-  const __amdgpu_buffer_rsrc_t r = buf_rsrc(cv, sizeof(ConvState));
-  auto ldi = [&](size_t off) { return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, kSc1); };
-  auto ldf = [&](size_t off) { return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, kSc1)); };
-  auto sti = [&](size_t off, int v) { __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, (int)off, 0, kSc1); };
-  auto stf = [&](size_t off, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, kSc1);
-  };
-  ConvState loc{};
-  loc.sum_current = ldf(offsetof(ConvState, sum_current));
-  loc.k = ldi(offsetof(ConvState, k));
-  loc.tol_count = ldi(offsetof(ConvState, tol_count));
-  loc.stopped = ldi(offsetof(ConvState, stopped));
-  loc.enabled = ldi(offsetof(ConvState, enabled));
-  loc.max_it = ldi(offsetof(ConvState, max_it));
-  loc.stag_max = ldi(offsetof(ConvState, stag_max));
-  loc.tol = ldf(offsetof(ConvState, tol));
-  loc.nonfinite_k = ldi(offsetof(ConvState, nonfinite_k));
-  loc.s_local = S;
-  residual_logic(&loc, S, hist_slot);
-  const uint64_t sb = __builtin_bit_cast(uint64_t, S);
-  sti(offsetof(ConvState, s_local), (int)(uint32_t)sb);
-  sti(offsetof(ConvState, s_local) + 4, (int)(uint32_t)(sb >> 32));
-  stf(offsetof(ConvState, residual), loc.residual);
-  stf(offsetof(ConvState, sum_current), loc.sum_current);
-  sti(offsetof(ConvState, k), loc.k);
-  sti(offsetof(ConvState, tol_count), loc.tol_count);
-  sti(offsetof(ConvState, stopped), loc.stopped);
-  sti(offsetof(ConvState, nonfinite_k), loc.nonfinite_k);
-  return loc.stopped;
-}
-
-// ctl[kCtlDone]: steps whose residual logic has run, | kDoneStop once a stop was decided
-constexpr int kDoneStop = 1 << 30;
-
-// The reducer workgroup (blockIdx.x == G): for each step, once all G workgroups have added
-// their arrival (each after its partial's sc1 store completed), sums the partials in
-// workgroup order, runs the residual logic and publishes the step count (with the stop bit)
-__device__ void co_reducer(const PersistArgs& p, double* red, int* sh) {
-  int* const ctl = p.ctl;
-  for (int s = 0; s < p.nsteps; ++s) {
-    if (threadIdx.x == 0) sh[0] = co_wait_geq(ctl + kCtlArr + (s & 3), p.G, ctl, p.timeout_ticks);
-    __syncthreads();
-    if (!sh[0]) return;
-    double t = 0.0;
-    for (int i = threadIdx.x; i < p.G; i += blockDim.x)
-      t += __hip_atomic_load(p.part + (size_t)(s & 3) * p.G + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = block_sum(t, red);
-    if (threadIdx.x == 0) {
-      const int stopped = co_residual(p.cv, t, p.hist ? p.hist + s : nullptr);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_agent(ctl + kCtlArr + (s & 3), 0);  // reused by step s + 4, after done >= s + 3
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_agent(ctl + kCtlDone, (s + 1) | (stopped ? kDoneStop : 0));
-      sh[0] = stopped;
-    }
-    __syncthreads();
-    if (sh[0]) return;
-  }
-}
-
-template <bool SW>
-__global__ __launch_bounds__(1024) void k_persist(const PersistArgs p) {
-  __shared__ double red[16];
-  __shared__ int sh[1];
-  const int w = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int* const ctl = p.ctl;
-  int* const flags = ctl + kCtlFlags;
-  if (threadIdx.x == 0) {  // a run stopped by an earlier call: nothing to do
-    const int k = ld_agent(&p.cv->k);
-    if (w == p.G) st_agent(ctl + kCtlK0, k);  // before this launch's first residual logic
-    sh[0] = ld_agent(&p.cv->stopped);
-  }
-  __syncthreads();
-  if (sh[0]) return;
-  if (w == p.G) {
-    co_reducer(p, red, sh);
-    return;
-  }
-  const int2 dp = p.deps[w];
-  const int nd = dp.y - dp.x + 1;  // <= 61 (host)
-  const int pos0 = w * p.m, pos1 = min(pos0 + p.m, p.nchunks);
-  for (int s = 0; s < p.nsteps; ++s) {
-    if (wave == 0) {
-      // one poll per round: lanes [0, nd) the flags of the workgroups this one pulls from
-      // (finished step s - 1), lane 63 the residual logic's step count (>= s - 1: at most one
-      // step runs ahead of a decision; a stop bit ends the launch), lane 62 the abort word
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int stop = 0;
-      for (;;) {
-        int ok = 1, quit = 0;
-        if (lane < nd) {
-          ok = ld_agent(flags + dp.x + lane) >= s;
-        } else if (lane == 63) {
-          const int d = ld_agent(ctl + kCtlDone);
-          ok = (d & (kDoneStop - 1)) >= s - 1;
-          quit = (d & kDoneStop) != 0;
-        } else if (lane == 62) {
-          quit = ld_agent(ctl + kCtlAbort) != 0;
-        }
-        if (__any(quit)) {
-          stop = 1;
-          break;
-        }
-        if (__all(ok)) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
-          if (lane == 0) st_agent(ctl + kCtlAbort, 1);
-          stop = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (lane == 0) sh[0] = stop;
-    }
-    __syncthreads();
-    if (sh[0]) break;
-    int si, di;
-    if (p.rot3) {
-      si = s % 3;
-      di = si == 2 ? 0 : si + 1;
-    } else {
-      si = (p.cur0 + s) & 1;
-      di = si ^ 1;
-    }
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(si == 0 ? p.buf0 : si == 1 ? p.buf1 : p.buf2, p.buf_bytes);
-    const __amdgpu_buffer_rsrc_t rd = buf_rsrc(di == 0 ? p.buf0 : di == 1 ? p.buf1 : p.buf2, p.buf_bytes);
-    const __amdgpu_buffer_rsrc_t rpi = buf_rsrc((s & 1) ? p.prev1 : p.prev0, p.prev_bytes);
-    const __amdgpu_buffer_rsrc_t rpo = buf_rsrc((s & 1) ? p.prev0 : p.prev1, p.prev_bytes);
-    const bool nee_active = p.h0 + s > 0;
-    double acc = 0.0;
-    const int pos = pos0 + (wave >> 2);
-    if (pos < pos1) {
-      const int ch = p.chunk0 >= 0 ? p.chunk0 + pos : p.chunks[pos];
-      acc = co_cell<SW>(p, rs, rd, rpi, rpo, ch * kChunk + (wave & 3) * 64 + lane, nee_active);
-    }
-    const double S = block_sum(acc, red);  // while the stores are in flight
-    if (threadIdx.x == 0)
-      __hip_atomic_store(p.part + (size_t)(s & 3) * p.G + w, S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores (and the partial) completed
-    __syncthreads();                                  // ... and every wave's
-    if (threadIdx.x == 0) {
-      st_agent(flags + w, s + 1);
-      __hip_atomic_fetch_add(ctl + kCtlArr + (s & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-__global__ void k_prev_fix(float4* prev0, const float4* __restrict__ prev1, int n, const ConvState* cv,
-                           const int* ctl) {
-  if (((cv->k - ctl[kCtlK0]) & 1) == 0) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) prev0[i] = prev1[i];
-}
-
 int grid_for(int64_t n, int block) {
   int64_t g = (n + block - 1) / block;
   if (g > 65536) g = 65536;
@@ -1395,27 +1093,6 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
     k = sw ? k_step<false, true> : k_step<false, false>;
   }
   hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_persist(const PersistArgs& p, hipStream_t s) {
-  if (p.G < 1 || p.m < 1 || p.m > 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(p.swap ? k_persist<true> : k_persist<false>, dim3(p.G + 1), dim3(kBlock * p.m), 0, s, p);
-  return hipGetLastError();
-}
-
-int persist_blocks_per_cu(int m, int swap) {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, swap ? k_persist<true> : k_persist<false>, kBlock * m, 0) !=
-      hipSuccess)
-    return 0;
-  return n;
-}
-
-hipError_t launch_prev_fix(float4* prev0, const float4* prev1, int n, const ConvState* cv, const int* ctl,
-                           hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prev_fix, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, s, prev0, prev1, n, cv, ctl);
   return hipGetLastError();
 }
 

@@ -125,60 +125,6 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
-
-// Persistent multi-step launch (k_persist; single domain, one cell per lane, small lattices):
-// ONE launch runs every step of an lbm_step call.  Workgroup w < G owns the active chunks at
-// list positions [w*m, min((w+1)*m, nchunks)) (256 threads per chunk) and the NEE-adjacent
-// cells among them.  Before step s it waits until the workgroups its pulls reach (deps[w] =
-// first, last) have finished step s - 1 (their flags) and until the residual logic of step
-// s - 2 has run (a stop decided there ends the launch).  Populations, NEE macros and the step
-// partials move with sc1 (L2-coherent, write-through) buffer loads and stores; a flag and an
-// arrival are published after every storing wave's stores have completed.  Workgroup G, the
-// reducer, sums each step's partials (fixed order) once all G arrived and runs the residual
-// logic.  The G + 1 workgroups must be co-resident (the host sizes the grid from the occupancy
-// query); the control words are zeroed before each launch; every wait gives up after
-// timeout_ticks (100 MHz) and raises ctl abort.
-enum : int { kCtlDone = 0, kCtlAbort = 1, kCtlK0 = 2, kCtlArr = 4, kCtlFlags = 16 };
-struct PersistArgs {
-  const float* buf0;    // population allocations (leading guard chunks included)
-  const float* buf1;
-  const float* buf2;    // rot3: step s reads buf[s % 3] and writes buf[(s + 1) % 3] (convergence
-  int rot3;             // control: a step run past the stop step then never overwrites the last
-                        // step's source, which the macro read-out needs); else buffers by parity
-  uint32_t buf_bytes;   // each (< 2 GiB: 32-bit buffer offsets)
-  int gfl;              // floats from an allocation's base to cell 0's chunk
-  int cur0;             // allocation holding the state at the call's start
-  const uint8_t* type;
-  const uint32_t* links;
-  const int* nee_of;    // per cell: its index in the NEE-adjacent list, or -1
-  const float* rho; const float* ux; const float* uy; const float* uz;  // NEE cells' boundary data
-  float4* prev0;        // NEE-adjacent cells' (rho, u): read at even steps of the call ...
-  float4* prev1;        // ... and at odd ones (k_prev_fix moves the final one into prev0)
-  uint32_t prev_bytes;
-  const uint2* nee_mask;
-  const float4* nee_bc;
-  const int* chunks; int chunk0; int nchunks;
-  int pitch; int plane;
-  int c_lo, c_hi;
-  float tau, tau_rcp, omc;
-  int tau_fast;
-  int h0;               // steps done before the call (NEE cells are raw pulls at step 0)
-  int nsteps;
-  int G, m;             // step workgroups (+ 1 reducer, all co-resident), chunks per workgroup (1, 2, 4)
-  const int2* deps;
-  ConvState* cv;
-  float* hist;          // nullable: per-step residual history of the call
-  int* ctl;             // kCtl* words, then G step flags
-  double* part;         // 4 x G step partials (ring by step)
-  uint64_t timeout_ticks;
-  int swap;
-};
-hipError_t launch_persist(const PersistArgs& p, hipStream_t s);
-// blocks of 256 * m threads k_persist can keep resident per CU (occupancy query)
-int persist_blocks_per_cu(int m, int swap);
-// after k_persist: prev0 = prev1 when the call ran an odd number of steps (cv->k - ctl[kCtlK0])
-hipError_t launch_prev_fix(float4* prev0, const float4* prev1, int n, const ConvState* cv, const int* ctl,
-                           hipStream_t s);
 constexpr int kNeeSlots = 5;  // NEE directions per cell whose data is gathered (one flat face: 5)
 // nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of mask[i].x
 hipError_t launch_nee_gather(const int* cells, const uint2* mask, const float* rho, const float* ux,

@@ -51,16 +51,12 @@ def knob(lbm):
         lbm.tune(which, prev)
 
 
-@pytest.fixture(params=["4", "1", "P"], ids=["4cells", "1cell", "persist"])
+@pytest.fixture(params=["4", "1"], ids=["4cells", "1cell"])
 def cells_per_lane(request, knob, lbm):
-    """Run a parity test through every stream-collide path: four cells per lane (the
-    bandwidth path), one cell per lane with one k_step1 launch per step, and one cell per
-    lane with one persistent k_persist launch per lbm_step call (what small single-domain
-    lattices use by default; larger ones and slabs fall back to k_step1)."""
-    cpl = 4 if request.param == "4" else 1
-    knob(lbm.TUNE_CELLS_PER_LANE, cpl)
-    knob(lbm.TUNE_PERSISTENT, 0 if request.param == "P" else 1)
-    return cpl
+    """Run a parity test through both stream-collide paths: four cells per lane (the
+    bandwidth path) and one cell per lane (what small lattices use by default)."""
+    knob(lbm.TUNE_CELLS_PER_LANE, int(request.param))
+    return int(request.param)
 
 
 @pytest.fixture(params=["x", "y"], ids=["xrows", "yrows"])
