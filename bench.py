@@ -134,6 +134,11 @@ def config_lines(dev: int):
     lat, geo, _, _ = cases.bifurcation(1, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
     out["bifurcation_64x83x32 (C4)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 2000)
+    # SURVEY 8(d) C4's bandwidth-relevant sparse number: the shipped mask upsampled 4x per axis
+    lat, raw = cases.bifurcation_upsampled(4, device=dev)
+    nl, _ = lbm_amd.index_transform(lat.geo())
+    out["bifurcation_x4_256x332x128 (C4 upsampled)"] = timed_mlups(lat, {"mlups_box": raw.size,
+                                                                         "mlups_nlattice": nl}, 200)
     # coronary.cu's 291 x 291 x 372 box with its five open ends on a synthetic vessel tree (the
     # reference's geo.txt is not shipped): a sparse lattice, 2.5 % of the box stored
     lat, geo = cases.coronary(cases.coronary_reference_vessel(), device=dev)

@@ -98,10 +98,10 @@ template <int Q, bool SW>
 __device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t cb, int64_t c,
                                            int pitch, int64_t plane) {
   const int64_t ro = row_off<Q, SW>(pitch, plane);
-  // plain loads: a line two chunks share (row straddles, the neighbour wave's edge float)
-  // more often still sits in the XCD's L2 when the second reader comes (non-temporal loads:
-  // 10.76 vs 10.58 GB HBM read per launch at 512^3, equal or 1% longer, r02 A/B)
-  a = *reinterpret_cast<const f4*>(src + aidx(c - ro, Q));
+  // non-temporal: every slice is read once per step.  Plain loads leave the lines two chunks
+  // share in L2 more often (10.58 vs 10.76 GB read per launch at 512^3, same time) but cost
+  // 7-10% at 256^3 and on C3 (interleaved A/B, profiles/r02_nt_vs_plain_ab.log)
+  a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + aidx(c - ro, Q)));
   if constexpr (SDir<Q, SW>::x == 1) e = src[aidx(cb - ro - 1, Q)];             // lane 0: b - 1
   else if constexpr (SDir<Q, SW>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];  // lane 63: b + 4
 }

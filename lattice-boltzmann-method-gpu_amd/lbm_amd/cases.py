@@ -158,6 +158,21 @@ def bifurcation_device(inlet_block: int = 0, geo_path: str | None = None, bc_pat
     return mask_device(raw.astype(np.uint8), inl, outl, device=device), raw
 
 
+def bifurcation_upsampled(k: int = 4, inlet_block: int = 1, geo_path: str | None = None,
+                          bc_path: str | None = None, device: int = 0):
+    """SURVEY 8(d) C4's bandwidth-relevant sparse variant: the shipped geo.txt mask nearest-
+    upsampled k times along every axis (k = 4: 256 x 332 x 128, ~4 M stored cells) and bc.txt's
+    inlet / outlet tables with it; geo_pre and initialize() on the device.  The default inlet
+    is block 1 (the block whose inlet drives a flow through the tree).  Returns (lat, raw)."""
+    geo_path = geo_path or os.path.join(BIF_DIR, "geo.txt")
+    bc_path = bc_path or os.path.join(BIF_DIR, "bc.txt")
+    raw = read_geo_txt(geo_path, BIF_SHAPE).astype(np.uint8)
+    _, inl, outl = read_bc_txt(bc_path, tuple(BIF_SHAPE), inlet_block)
+    up = np.ascontiguousarray(raw.repeat(k, 0).repeat(k, 1).repeat(k, 2))
+    big = [np.ascontiguousarray(t.repeat(k, 0).repeat(k, 1)) for t in (inl, outl)]
+    return mask_device(up, big[0], big[1], device=device), up
+
+
 def coronary_bc_codes(c_u: float = 2.74909090909091):
     """The boundary codes of coronary.cu's boundary_stream (716-944) as LBM_CASE_GENERIC entries:
     code 2 inlet (fluid at x+1): u_bc = (0.1745/C_U, 0, 0), rho_bc = 1;

@@ -119,3 +119,29 @@ def test_device_mask_slabs(gpu, nslabs, row_axis):
     for z0, z1, lat in slabs:
         for a, b in zip(lat.macros(), ref):
             assert np.array_equal(a.view(np.uint32), b[z0:z1].view(np.uint32))
+
+
+def test_bifurcation_upsampled_bitwise(gpu, oracle):
+    """SURVEY 8(d) C4's bandwidth-relevant sparse variant (the shipped mask upsampled 4x per
+    axis, 256 x 332 x 128, ~4 M stored cells; the bench's secondary line): device codes equal the
+    oracle's geo_pre, and the lattice steps bit for bit like the oracle."""
+    from lbm_amd import cases, index_transform
+    lat, up = cases.bifurcation_upsampled(4)
+    geo = oracle.geo_mask(up.astype(np.int32))
+    got = lat.geo()
+    assert np.array_equal(got, geo), f"{np.count_nonzero(got != geo)} codes differ"
+    nl, _ = index_transform(geo)
+    assert 3_500_000 < nl < 4_500_000, nl  # "~4 M stored cells" (SURVEY 8(d))
+    from lbm_amd import read_bc_txt, BIF_SHAPE
+    import os
+    _, inl, outl = read_bc_txt(os.path.join(cases.BIF_DIR, "bc.txt"), tuple(BIF_SHAPE), 1)
+    inl4 = inl.repeat(4, 0).repeat(4, 1)
+    outl4 = outl.repeat(4, 0).repeat(4, 1)
+    inl_m = np.where(geo[:, 1, :] == 2, inl4, 0).astype(np.float32)
+    outl_m = np.where(geo[:, -2, :] == 3, outl4, 0).astype(np.float32)
+    o = oracle.Oracle(oracle.MASK, geo, 0.55, inlet_uy=inl_m, outlet_uy=outl_m)
+    for s in (1, 9):
+        lat.step(s)
+        o.step(s)
+        assert_bitwise(lat, o, geo, 2, f"bif x4 +{s}")
+    assert o.bad_reads() == 0
