@@ -417,6 +417,41 @@ __device__ __forceinline__ void nee_pull_all(float* f, const MainArgs& a, int64_
   (nee_put<Qs, SW>(f, nv, a, c, mp, nee, m.y), ...);
 }
 
+// Cells beside one flat boundary face (nearly all NEE-adjacent cells; the list is grouped by
+// direction mask, so whole waves share one) take all five directions of that face: the
+// j-th direction is a compile-time q, the NEE value the compile-time feq_bc<q> / feq<q> trees
+// (the same expressions feq_rt evaluates at run time), and no slot selection is needed.
+constexpr bool crosses_face(int q, int f) {
+  const int e = f < 2 ? kEx[q] : f < 4 ? kEy[q] : kEz[q];
+  return e == ((f & 1) ? -1 : 1);
+}
+constexpr int face_q(int f, int j) {  // the j-th (ascending) direction crossing face f
+  int k = 0;
+  for (int q = 1; q < kQ; ++q)
+    if (crosses_face(q, f)) {
+      if (k == j) return q;
+      ++k;
+    }
+  return 0;
+}
+constexpr uint32_t face_set(int f) {
+  uint32_t m = 0;
+  for (int q = 1; q < kQ; ++q)
+    if (crosses_face(q, f)) m |= 1u << q;
+  return m;
+}
+
+template <int F, bool SW, int... Js, int... Qs>
+__device__ __forceinline__ void nee_pull_face(float* f, const MainArgs& a, int64_t c, const Macro& mp, uint32_t press,
+                                              const float4* bc, std::integer_sequence<int, Js...>,
+                                              std::integer_sequence<int, Qs...>) {
+  float own[kNeeSlots];
+  ((own[Js] = a.src[aidx(c, face_q(F, Js))]), ...);
+  ((f[Qs] = a.src[aidx(c - cell_off<Qs, SW>(a.pitch, a.plane), Qs)]), ...);
+  ((f[face_q(F, Js)] = nee_value<face_q(F, Js)>(nee_slot(own[Js], bc[Js]), mp, (press >> face_q(F, Js)) & 1u, a.omc)),
+   ...);
+}
+
 template <int... Qs>
 __device__ __forceinline__ void fix_relax_all(float* f, float tau, float r, float ux, float uy, float uz,
                                               std::integer_sequence<int, Qs...>) {
@@ -472,7 +507,19 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   for (int j = 0; j < kNeeSlots; ++j) bc[j] = a.nee_bc[(int64_t)i * kNeeSlots + j];
   const uint32_t links = a.links[c];
   float f[kQ];
-  nee_pull_all<SW>(f, a, c, mp, mk, bc, AllQ{});
+  // a wave whose cells all sit beside one flat y face -- the reference's lid (ldc.cu:391-456),
+  // inlet and outlet (Poiseulle.cu:748-891, bifurcation.cu:877-1021) -- takes that face's
+  // specialised path.  Only the two y faces: the step kernels are latency-bound at the sizes
+  // where NEE cells matter, and six specialisations grew k_step1 by half and gave the
+  // bifurcation's gain back (C4 10.8 vs 11.7 us per step, LDC 64^3 11.9 either way); one
+  // shared moments / relaxation tail for fluid and NEE cells was slower too (12.3 / 10.9 us).
+  const uint32_t nee = a.nee_active ? mk.x : 0u;
+  const uint32_t nee0 = __builtin_amdgcn_readfirstlane(nee);
+  const bool uniform = __all(nee == nee0);
+  using Five = std::make_integer_sequence<int, kNeeSlots>;
+  if (uniform && nee0 == face_set(kFacePY)) nee_pull_face<kFacePY, SW>(f, a, c, mp, mk.y, bc, Five{}, AllQ{});
+  else if (uniform && nee0 == face_set(kFaceNY)) nee_pull_face<kFaceNY, SW>(f, a, c, mp, mk.y, bc, Five{}, AllQ{});
+  else nee_pull_all<SW>(f, a, c, mp, mk, bc, AllQ{});
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
