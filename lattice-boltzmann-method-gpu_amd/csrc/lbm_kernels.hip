@@ -540,14 +540,31 @@ __device__ __forceinline__ void pull1_all(float* f, const float* __restrict__ sr
   ((f[Qs] = __builtin_nontemporal_load(src + aidx(c - cell_off<Qs, SW>(pitch, plane), Qs))), ...);
 }
 
+// The same pulls for a wave whose cells all lie in chunk ch (lane cell ch * 256 + l): a
+// wave-uniform base W chunks below ch and 32-bit lane offsets (W * 256 >= plane + pitch + 1
+// keeps them non-negative) -- 5 VALU per pull instead of the 64-bit aidx's 10; the one-cell
+// waves of small lattices are VALU-bound
+__device__ __forceinline__ uint32_t rel_aidx(int r, int q) {
+  return (uint32_t)(((r >> 8) * kQ + q) * kChunk + (r & (kChunk - 1)));
+}
+template <bool SW, int... Qs>
+__device__ __forceinline__ void pull1w_all(float* f, const float* __restrict__ src, int64_t ch, int l, int pitch,
+                                           int64_t plane, std::integer_sequence<int, Qs...>) {
+  const int W = (int)((plane + pitch + 1) >> 8) + 2;
+  const float* base = src + (ch - W) * (kQ * kChunk);
+  const int r0 = l + W * kChunk;
+  ((f[Qs] = __builtin_nontemporal_load(base + rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs))), ...);
+}
+
 template <bool SW>
-__device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t c) {
+__device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, int l) {
   // the pulls go out with the type byte (one round trip; the guard chunks keep every
   // address of a lane that turns out to be idle inside the buffer)
+  const int64_t c = ch * kChunk + l;
   const uint8_t t = a.type[c];
   const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
   float f[kQ];
-  pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
+  pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
   const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid &&
                   !(t & kNeedsMac);
   if (!in) return 0.0;
@@ -617,7 +634,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     const int idx = slot * (kBlock / 64) + wave;
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
-        acc = process_cell1<SW>(a, chunk_of(a, idx >> 2) * kChunk + (idx & 3) * 64 + lane);
+        acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
     } else if (idx < a.nchunks) {
       acc = process_chunk<FAST, SW>(a, chunk_of(a, idx) * kChunk, lane);  // uniform base
     }
