@@ -246,7 +246,8 @@ def main():
 
     # attainable streaming bandwidth of this device, same run (context for roofline.frac:
     # the 8 TB/s spec peak is not reached by any kernel)
-    probe = round(lbm_amd.probe_stream(local), 1) if rank == 0 else None
+    probe_shapes = lbm_amd.probe_stream_shapes(local) if rank == 0 else None
+    probe = max(probe_shapes.values()) if probe_shapes else None
 
     if rank != 0:
         if world > 1:
@@ -306,10 +307,11 @@ def main():
             "boundary_cells_per_gpu": counts["n_boundary"],
             "stream_probe_gbs": probe,
             "frac_of_stream_probe": round(achieved / probe, 4) if probe else None,
-            "stream_probe": "lbm_probe_stream: best of 9 streaming-copy shapes (16-B vectors, grid-stride, "
-                            "per-XCD regions or k_step-like 16-KB wave tiles, plain or non-temporal; read + write bytes / time) between the two "
-                            "fastest-writing of up to six 8-GiB allocations (the population buffers' placement "
-                            "rule) on this GPU in this run",
+            "stream_probe": "lbm_probe_stream: best of 11 streaming-copy shapes (16-B vectors, grid-stride, "
+                            "per-XCD regions or k_step-like 16-KB wave tiles, plain or non-temporal, the tiles also by "
+                            "LDS-DMA; read + write bytes / time) between the two fastest-writing of up to six 8-GiB "
+                            "allocations (the population buffers' placement rule) on this GPU in this run",
+            "stream_probe_shapes_gbs": probe_shapes,
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
         "step_kernel_ms_by_source_buffer": parity_ms,

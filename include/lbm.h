@@ -261,12 +261,16 @@ int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
 /* Measurement helper (not a reference interface): the HBM rate a plain streaming copy
  * reaches on this device, for context next to k_step's roofline fraction.  Copies `bytes`
  * (rounded down to 64 KiB) between two device buffers with 16-B loads and stores in a few
- * shapes (grid-stride or one contiguous region per XCD, plain or non-temporal, and k_step's own:
- * one wave per 16-KB tile with all 16 loads per lane in flight), `reps` timed
+ * shapes (grid-stride or one contiguous region per XCD, plain or non-temporal, k_step's own:
+ * one wave per 16-KB tile with all 16 loads per lane in flight, and that tile by LDS-DMA), `reps` timed
  * launches each (HIP events, after one untimed launch); *gbs = the best (read + write bytes) /
  * duration in GB/s.  The two buffers are picked as the population buffers are
  * (lbm_buffer_placement): the two fastest-writing of up to six allocations of `bytes`. */
 int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs);
+/* The same, per copy shape: gbs_shape[i] = the best rate of shape i for i < min(cap, n);
+ * *n = the number of shapes (grid-stride / per-XCD-region copies, k_step's 16-KB wave tiles by
+ * plain or non-temporal 16-B loads, the same tiles by LDS-DMA, global_load_lds). */
+int lbm_probe_stream_shapes(int device, int64_t bytes, int reps, double* gbs_shape, int cap, int* n);
 
 /* Multi-GPU z-slabs (one process per GPU).  Rank 0 calls lbm_rccl_unique_id, the 128 bytes
  * are broadcast by the caller (e.g. torch.distributed), then every rank attaches.  After

@@ -1443,7 +1443,20 @@ int lbm_stats(lbm_ctx* c, double* kernel_ms, int64_t* launches, double* algo_byt
 }
 
 int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
-  if (bytes < (1 << 16) || reps < 1 || !gbs) {
+  if (!gbs) {
+    g_create_error = "lbm_probe_stream: gbs non-null";
+    return LBM_ERR_ARG;
+  }
+  double per[16] = {};
+  int n = 0;
+  const int rc = lbm_probe_stream_shapes(device, bytes, reps, per, 16, &n);
+  *gbs = 0.0;
+  for (int i = 0; i < n && i < 16; ++i) *gbs = std::max(*gbs, per[i]);
+  return rc;
+}
+
+int lbm_probe_stream_shapes(int device, int64_t bytes, int reps, double* gbs_shape, int cap, int* nshapes) {
+  if (bytes < (1 << 16) || reps < 1 || !gbs_shape || cap < 0) {
     g_create_error = "lbm_probe_stream: bytes >= 64 KiB, reps >= 1, gbs non-null";
     return LBM_ERR_ARG;
   }
@@ -1451,7 +1464,6 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
   void *a = nullptr, *b = nullptr;
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  double best = 0.0;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&e0);
@@ -1495,8 +1507,13 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
     }
     if (e == hipSuccess && (!a || !b)) e = hipErrorOutOfMemory;
   }
-  const int shapes[][2] = {{8192, 0}, {8192, 1}, {8192, 2}, {8192, 3}, {4096, 4}, {2048, 5}, {32768, 2}, {0, 6}, {0, 7}};
-  for (const auto& sh : shapes) {  // blocks, launch_probe_copy shape
+  const int shapes[][2] = {{8192, 0}, {8192, 1}, {8192, 2}, {8192, 3}, {4096, 4}, {2048, 5}, {32768, 2},
+                           {0, 6},    {0, 7},    {0, 8},    {0, 9}};
+  const int nsh = (int)(sizeof(shapes) / sizeof(shapes[0]));
+  if (nshapes) *nshapes = nsh;
+  for (int i = 0; i < cap; ++i) gbs_shape[i] = 0.0;
+  for (int si = 0; si < nsh; ++si) {  // blocks, launch_probe_copy shape
+    const auto& sh = shapes[si];
     if (e != hipSuccess) break;
     e = launch_probe_copy(a, b, n4, sh[0], sh[1], st);  // untimed first launch
     for (int r = 0; r < reps && e == hipSuccess; ++r) {
@@ -1506,7 +1523,8 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
       if (e == hipSuccess) e = hipEventSynchronize(e1);
       float ms = 0.f;
       if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-      if (e == hipSuccess && ms > 0.f) best = std::max(best, 2.0 * 16.0 * (double)n4 / (ms * 1e-3) / 1e9);
+      if (e == hipSuccess && ms > 0.f && si < cap)
+        gbs_shape[si] = std::max(gbs_shape[si], 2.0 * 16.0 * (double)n4 / (ms * 1e-3) / 1e9);
     }
   }
   if (e != hipSuccess) g_create_error = std::string("lbm_probe_stream: ") + hipGetErrorString(e);
@@ -1515,7 +1533,6 @@ int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs) {
   if (st) (void)hipStreamDestroy(st);
   if (a) (void)hipFree(a);
   if (b) (void)hipFree(b);
-  *gbs = best;
   return e == hipSuccess ? LBM_OK : LBM_ERR_HIP;
 }
 

@@ -160,8 +160,9 @@ hipError_t launch_prev_scatter(const int* cells, const float4* prev, int n, floa
 // grid-stride non-temporal / plain, 2/3 the same with one contiguous region per XCD, 4/5
 // XCD regions with 2 / 4 vectors in flight per thread; 6/7 k_step's shape (non-temporal /
 // plain): one wave per 16-KB tile, 16 vectors per lane in flight, tiles in contiguous runs per
-// XCD, `blocks` ignored (n4 must be a multiple of 4096)
-constexpr int kProbeShapes = 8;
+// XCD, `blocks` ignored (n4 must be a multiple of 4096); 8/9 the same tiles loaded by LDS-DMA
+// (non-temporal / default policy)
+constexpr int kProbeShapes = 10;
 hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks, int shape, hipStream_t s);
 // zero n4 16-B vectors with one sweep of non-temporal stores (one region per XCD): the write
 // rate buffer_placement ranks allocations by

@@ -86,7 +86,7 @@ LBM_SYMBOLS = [
     "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
     "lbm_get_layout", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
-    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream",
+    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
 ]
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
@@ -189,6 +189,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_comm_info": (C.c_int, [P, ip, ip]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
             "lbm_probe_stream": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p]),
+            "lbm_probe_stream_shapes": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p, C.c_int, ip]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -575,14 +576,26 @@ class Lattice:
         self._ck(lbm_lib().lbm_attach_rccl(self.h, buf, rank, nranks), "lbm_attach_rccl")
 
 
+# lbm_probe_stream_shapes' copy shapes, in order (lbm_kernels.hpp launch_probe_copy)
+PROBE_SHAPES = ["grid_nt", "grid", "xcd_nt", "xcd", "xcd_nt_x2", "xcd_nt_x4", "xcd_nt_32k_blocks", "tiles_nt",
+                "tiles", "tiles_ldsdma_nt", "tiles_ldsdma"]
+
+
+def probe_stream_shapes(device: int = 0, nbytes: int = 8 << 30, reps: int = 5) -> dict:
+    """Streaming-copy rate (read + write GB/s) of every copy shape (lbm_probe_stream_shapes)."""
+    per = (C.c_double * 32)()
+    n = C.c_int()
+    rc = lbm_lib().lbm_probe_stream_shapes(device, nbytes, reps, per, 32, C.byref(n))
+    if rc != 0:
+        raise LbmError(f"lbm_probe_stream: {lbm_lib().lbm_last_error(None).decode()}")
+    names = PROBE_SHAPES + [f"shape{i}" for i in range(len(PROBE_SHAPES), n.value)]
+    return {names[i]: round(per[i], 1) for i in range(min(n.value, 32))}
+
+
 def probe_stream(device: int = 0, nbytes: int = 8 << 30, reps: int = 5) -> float:
     """Best streaming-copy rate (read + write GB/s) of the device (lbm_probe_stream): the
     attainable HBM bandwidth next to the 8 TB/s spec peak."""
-    gbs = C.c_double()
-    rc = lbm_lib().lbm_probe_stream(device, nbytes, reps, C.byref(gbs))
-    if rc != 0:
-        raise LbmError(f"lbm_probe_stream: {lbm_lib().lbm_last_error(None).decode()}")
-    return gbs.value
+    return max(probe_stream_shapes(device, nbytes, reps).values())
 
 
 def rccl_unique_id() -> bytes:
