@@ -1220,6 +1220,29 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const f4* __restrict__ a, f
   }
 }
 
+// The same tiles moved by LDS-DMA (global_load_lds, 16 B per lane: the loads take no VGPRs, so
+// a wave keeps its whole 16-KB tile in flight in LDS; two 64-KB workgroups per CU), then
+// ds_read_b128 + stores; NT: the loads' non-temporal policy (MI355X_MICROARCH.md, ldsdma-fill)
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+template <bool NT>
+__global__ __launch_bounds__(256) void k_probe_lds(const f4* __restrict__ a, f4* __restrict__ b, int64_t ntiles) {
+  __shared__ f4 tile[4][1024];
+  const int64_t nb = gridDim.x;  // a multiple of 8
+  const int64_t lb = (int64_t)(blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t = lb * 4 + w;
+  if (t >= ntiles) return;
+  const f4* src = a + t * 1024;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + k * 64 + lane), (lds_ptr_t)&tile[w][k * 64], 16, 0,
+                                     NT ? 2 : 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's own tile: no barrier needed
+#pragma unroll
+  for (int k = 0; k < 16; ++k) __builtin_nontemporal_store(tile[w][k * 64 + lane], b + t * 1024 + k * 64 + lane);
+}
+
 hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks, int shape, hipStream_t s) {
   const f4* a = static_cast<const f4*>(src);
   f4* b = static_cast<f4*>(dst);
@@ -1228,7 +1251,9 @@ hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks,
     const int64_t ntiles = n4 / 1024;
     const unsigned grid = (unsigned)((ntiles / 4 + 7) / 8 * 8);
     if (shape == 6) hipLaunchKernelGGL((k_probe_tiles<true>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
-    else hipLaunchKernelGGL((k_probe_tiles<false>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
+    else if (shape == 7) hipLaunchKernelGGL((k_probe_tiles<false>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
+    else if (shape == 8) hipLaunchKernelGGL((k_probe_lds<true>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
+    else hipLaunchKernelGGL((k_probe_lds<false>), dim3(grid), dim3(256), 0, s, a, b, ntiles);
     return hipGetLastError();
   }
   switch (shape) {
