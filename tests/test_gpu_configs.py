@@ -129,3 +129,14 @@ def test_nan_guard(gpu, oracle):
         else:
             assert st["k"] == 20
         lat.close()
+
+
+def test_probe_stream_shapes(gpu):
+    """lbm_probe_stream_shapes: a rate for every copy shape (register and LDS-DMA tiles
+    included), and lbm_probe_stream reports their best."""
+    import lbm_amd
+    per = lbm_amd.probe_stream_shapes(0, 256 << 20, 2)
+    assert list(per) == lbm_amd.PROBE_SHAPES, per
+    assert all(v > 0 for v in per.values()), per
+    best = lbm_amd.probe_stream(0, 256 << 20, 2)
+    assert 0.5 * max(per.values()) < best < 2.0 * max(per.values())
