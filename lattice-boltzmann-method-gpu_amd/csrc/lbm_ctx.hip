@@ -60,6 +60,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   float4* prev = nullptr; // their (rho, u) of the previous step
   uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
   float4* nee_bc = nullptr;   // their first kNeeSlots NEE neighbours' boundary data (static)
+  unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
   int main_blocks = 0, nee_blocks = 0, nee_waves = 4;
@@ -307,6 +308,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, int srcbuf, hipStream_t st, const
   a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
   a.partial = r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
+  a.lane_masks = r.quarter ? nullptr : r.lane_masks;
   a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.tau = c->tau;
@@ -434,6 +436,33 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     const int cpl = g_tune[LBM_TUNE_CELLS_PER_LANE];  // A/B switch: 1 or 4 (0: by size)
     r.quarter = cpl ? (cpl == 1) : (r.nchunks <= kQuarterMaxChunks);
   }
+  // Lane masks for the 4-cell path: bit l of a chunk's mask is set when lane l (cells 4l ..
+  // 4l+3) holds a cell the chunk wave updates (fluid, in range, not NEE-adjacent) or neighbours
+  // such a lane (the DPP x-shift reads the next lanes' slices).  Lanes outside it load nothing:
+  // on a vessel tree most chunks are partly empty (the upsampled bifurcation keeps 51% of its
+  // active chunks' cells).  Only for sparse chunk lists, whose waves load their chunk id
+  // anyway (the mask load goes out beside it); a contiguous list would pay a round trip.
+  if (!r.quarter && r.nchunks && r.chunk0 < 0) {
+    std::vector<unsigned long long> lm(chunks.size());
+    bool partial = false;
+    for (size_t j = 0; j < chunks.size(); ++j) {
+      unsigned long long m = 0;
+      const int64_t base = (int64_t)chunks[j] * kChunk;
+      for (int l = 0; l < 64; ++l)
+        for (int k = 0; k < 4; ++k) {
+          const int64_t cell = base + 4 * l + k;
+          const uint8_t v = t[cell];
+          if (in(cell) && (v & kClassMask) == kFluid && !(v & kNeedsMac)) m |= 1ull << l;
+        }
+      m |= (m << 1) | (m >> 1);
+      lm[j] = m;
+      partial |= m != ~0ull;
+    }
+    if (partial) {
+      HIPCK(c, hipMalloc(&r.lane_masks, sizeof(unsigned long long) * lm.size()));
+      HIPCK(c, hipMemcpy(r.lane_masks, lm.data(), sizeof(unsigned long long) * lm.size(), hipMemcpyHostToDevice));
+    }
+  }
   r.main_blocks = main_grid(r.nchunks, r.quarter);
   r.nee_waves = nee_waves_for(r.nslow, contig);
   r.nee_blocks = nee_grid(r.nslow, r.nee_waves);
@@ -443,6 +472,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
 
 void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
+  if (r.lane_masks) (void)hipFree(r.lane_masks);
   if (r.cells) (void)hipFree(r.cells);
   if (r.prev) (void)hipFree(r.prev);
   if (r.nee_mask) (void)hipFree(r.nee_mask);

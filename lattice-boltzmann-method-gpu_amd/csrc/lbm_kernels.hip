@@ -96,12 +96,16 @@ constexpr int64_t cell_off(int pitch, int64_t plane) {
 //           lane 0 (e_x = +1) or lane 63 (e_x = -1).
 template <int Q, bool SW>
 __device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t cb, int64_t c,
-                                           int pitch, int64_t plane) {
+                                           int pitch, int64_t plane, bool need) {
   const int64_t ro = row_off<Q, SW>(pitch, plane);
+  // lanes outside the chunk's lane mask (sparse lattices) all read the buffer's first line,
+  // which stays cached: no HBM bytes for them, and no branch (a branch per direction made the
+  // compiler wait for every load before issuing the next)
+  const float* p = need ? src + aidx(c - ro, Q) : src;
   // non-temporal: every slice is read once per step.  Plain loads leave the lines two chunks
   // share in L2 more often (10.58 vs 10.76 GB read per launch at 512^3, same time) but cost
   // 7-10% at 256^3 and on C3 (interleaved A/B, profiles/r02_nt_vs_plain_ab.log)
-  a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + aidx(c - ro, Q)));
+  a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
   if constexpr (SDir<Q, SW>::x == 1) e = src[aidx(cb - ro - 1, Q)];             // lane 0: b - 1
   else if constexpr (SDir<Q, SW>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];  // lane 63: b + 4
 }
@@ -121,9 +125,9 @@ __device__ __forceinline__ f4 pull_compose(const f4 a, float e, int lane) {
 
 template <bool SW, int... Qs>
 __device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t cb, int64_t c, int lane,
-                                          int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
+                                          int pitch, int64_t plane, bool need, std::integer_sequence<int, Qs...>) {
   float e[kQ];
-  ((pull_issue<Qs, SW>(v[Qs], e[Qs], src, cb, c, pitch, plane)), ...);
+  ((pull_issue<Qs, SW>(v[Qs], e[Qs], src, cb, c, pitch, plane, need)), ...);
   ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], lane)), ...);
 }
 
@@ -220,13 +224,17 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
 //        branch) the exact division, counted in exact_waves.  Both paths cost 216 VGPRs
 //        against 170 for one -- no occupancy change, since the LDS reservation already
 //        holds the kernel at two waves per SIMD.
-template <bool FAST, bool SW>
-__device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane) {
+template <bool FAST, bool SW, bool MASK>
+__device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
   double acc = 0.0;
   const int64_t c = cb + lane * 4;
+  // lanes the chunk's mask leaves out hold no fluid cell and neighbour none: they load nothing
+  // and count as passive (nothing stored, no |u|)
+  const bool need = MASK ? ((lane_mask >> lane) & 1u) != 0 : true;
   f4 v[kQ];
-  pull4_all<SW>(v, a.src, cb, c, lane, a.pitch, a.plane, AllQ{});
-  const unsigned t4 = *reinterpret_cast<const unsigned*>(a.type + c);
+  pull4_all<SW>(v, a.src, cb, c, lane, a.pitch, a.plane, need, AllQ{});
+  const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
+  const unsigned t4 = need ? t4r : 0u;
   // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
   // so this dependent load hides behind the arithmetic)
   constexpr unsigned kWall4 = kWallAdj * 0x01010101u;
@@ -604,7 +612,7 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
   return a.chunk0 >= 0 ? (int64_t)a.chunk0 + idx : (int64_t)a.chunks[idx];
 }
 
-template <bool FAST, bool QUARTER, bool SW>
+template <bool FAST, bool QUARTER, bool SW, bool MASK = false>
 __device__ __forceinline__ void step_body(const MainArgs& a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -636,7 +644,8 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       if ((idx >> 2) < a.nchunks)
         acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
     } else if (idx < a.nchunks) {
-      acc = process_chunk<FAST, SW>(a, chunk_of(a, idx) * kChunk, lane);  // uniform base
+      const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
+      acc = process_chunk<FAST, SW, MASK>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base
     }
     slot += a.red_blocks + a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
@@ -650,9 +659,9 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
 }
 
 // 4 cells per lane (big lattices): two waves per SIMD, pinned by the LDS reservation
-template <bool FAST, bool SW>
+template <bool FAST, bool SW, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
-  step_body<FAST, false, SW>(a);
+  step_body<FAST, false, SW, MASK>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
 template <bool SW>
@@ -1153,9 +1162,11 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
     k = sw ? k_step1<true> : k_step1<false>;
   } else if (a.fast_div) {
-    k = sw ? k_step<true, true> : k_step<true, false>;
+    if (a.lane_masks) k = sw ? k_step<true, true, true> : k_step<true, false, true>;
+    else k = sw ? k_step<true, true, false> : k_step<true, false, false>;
   } else {
-    k = sw ? k_step<false, true> : k_step<false, false>;
+    if (a.lane_masks) k = sw ? k_step<false, true, true> : k_step<false, false, true>;
+    else k = sw ? k_step<false, true, false> : k_step<false, false, false>;
   }
   hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, a);
   return hipGetLastError();

@@ -63,6 +63,9 @@ struct MainArgs {
   int chunk0;           // >= 0: they are chunk0, chunk0 + 1, ... (box lattices) -- no list load,
                         // one dependent round trip less per wave
   int nchunks;
+  const unsigned long long* lane_masks;  // nullable (4-cell path): per chunk of the list, bit l set when
+                        // lane l (cells 4l .. 4l+3) or a neighbouring lane holds a cell the chunk
+                        // wave updates; the other lanes load nothing (sparse lattices)
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
   int quarter;          // 1: one cell per lane, a wave per 64-cell quarter chunk (small lattices)
   int pitch;

@@ -287,7 +287,9 @@ def test_fast_division_retry_large(gpu, oracle):
     lat, geo = cases.ldc(n)
     o = oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE)
     f = o.f()
-    f[5, 100, n - 3, 17] = 1e-30
+    # each pulled by a chunk-wave fluid cell (y = n - 3 would be NEE-adjacent, under the lid:
+    # the NEE blocks update it and the chunk wave's lane mask leaves it out)
+    f[5, 100, n - 4, 17] = 1e-30
     f[7, 2, 140, 2] = 3e-25
     f[11, 200, 60, 201] = 7e-39
     lat.set_f(f)
