@@ -221,9 +221,8 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.  NEE-adjacent cells
 // are left to the NEE blocks of the same launch (nee_cell).
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
-//        branch) the exact division, counted in exact_waves.  Both paths cost 216 VGPRs
-//        against 170 for one -- no occupancy change, since the LDS reservation already
-//        holds the kernel at two waves per SIMD.
+//        branch) the exact division, counted in exact_waves.  Both paths cost 216-220 VGPRs
+//        against 170 for one -- no occupancy change: either way two waves per SIMD.
 template <bool FAST, bool SW, bool MASK>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
   double acc = 0.0;
@@ -550,8 +549,8 @@ __device__ __forceinline__ void pull1_all(float* f, const float* __restrict__ sr
 
 // The same pulls for a wave whose cells all lie in chunk ch (lane cell ch * 256 + l): a
 // wave-uniform base W chunks below ch and 32-bit lane offsets (W * 256 >= plane + pitch + 1
-// keeps them non-negative) -- 5 VALU per pull instead of the 64-bit aidx's 10; the one-cell
-// waves of small lattices are VALU-bound
+// keeps them non-negative) -- 6 VALU per pull instead of the 64-bit aidx's ~10 (C4 10.8 ->
+// 10.7 us per step, LDC 64^3 unchanged: the small lattices' chain is mostly latency)
 __device__ __forceinline__ uint32_t rel_aidx(int r, int q) {
   return (uint32_t)(((r >> 8) * kQ + q) * kChunk + (r & (kChunk - 1)));
 }
@@ -658,7 +657,8 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
   if (threadIdx.x == 0) a.partial[slot] = s;
 }
 
-// 4 cells per lane (big lattices): two waves per SIMD, pinned by the LDS reservation
+// 4 cells per lane (big lattices): two waves per SIMD (216-220 VGPRs); MASK: the range has
+// lane masks (sparse chunk lists)
 template <bool FAST, bool SW, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
   step_body<FAST, false, SW, MASK>(a);
