@@ -6,7 +6,7 @@
 //
 //  k_step, chunk blocks  one wavefront per 256-cell AoSoA chunk, 4 consecutive cells per
 //                    lane: 19 aligned 16-B pulls issued at once (x neighbours by a DPP lane
-//                    shift, the edge lanes' floats by wave-uniform scalar loads), moments,
+//                    shift, the edge lanes' floats by vector loads that often hit L1), moments,
 //                    equilibria and BGK relaxation in registers, 19 16-B stores into the
 //                    chunk.  Half-way bounce-back costs no extra pass and no extra round
 //                    trip: a wall-adjacent cell also stores its outgoing population opp(q)
@@ -90,8 +90,8 @@ constexpr int64_t cell_off(int pitch, int64_t plane) {
 // Pull of population Q for the lane's 4 cells c..c+3 from c - e_Q .. c+3 - e_Q, in two
 // phases so that all of a wave's loads are in flight together (one round trip per wave):
 //  issue:   the aligned 16-B slice at c - (e_Q with e_x = 0), and for e_x != 0 the one
-//           float the wave's edge lane needs from the neighbouring chunk -- a wave-uniform
-//           address (chunk base cb), so a scalar load with no branch;
+//           float the wave's edge lane needs from the neighbouring chunk (all lanes load the
+//           same address, no branch);
 //  compose: shift the slice by one cell across lanes (DPP) and drop the edge float into
 //           lane 0 (e_x = +1) or lane 63 (e_x = -1).
 template <int Q, bool SW>
@@ -106,8 +106,21 @@ __device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restr
   // share in L2 more often (10.58 vs 10.76 GB read per launch at 512^3, same time) but cost
   // 7-10% at 256^3 and on C3 (interleaved A/B, profiles/r02_nt_vs_plain_ab.log)
   a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
-  if constexpr (SDir<Q, SW>::x == 1) e = src[aidx(cb - ro - 1, Q)];             // lane 0: b - 1
-  else if constexpr (SDir<Q, SW>::x == -1) e = src[aidx(cb + kChunk - ro, Q)];  // lane 63: b + 4
+  // The edge float by a VECTOR load: its line is the neighbouring chunk's slice, which the
+  // neighbouring wave -- three times in four a wave of this block, on this CU -- loads at the
+  // same time, so it often hits this CU's L1; a wave-uniform address would make it a scalar
+  // load, which only the scalar cache and L2 serve (0.30 GB less HBM read per launch at 512^3,
+  // +1.8-2.7% in interleaved A/B runs, profiles/r02_edge_vector_ab.log).  The empty asm moves
+  // the offset to a VGPR.
+  if constexpr (SDir<Q, SW>::x == 1) {  // lane 0: b - 1
+    int64_t o = aidx(cb - ro - 1, Q);
+    asm volatile("" : "+v"(o));
+    e = src[o];
+  } else if constexpr (SDir<Q, SW>::x == -1) {  // lane 63: b + 4
+    int64_t o = aidx(cb + kChunk - ro, Q);
+    asm volatile("" : "+v"(o));
+    e = src[o];
+  }
 }
 
 template <int Q, bool SW>

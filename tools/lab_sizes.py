@@ -12,14 +12,15 @@ import torch  # noqa: E402,F401
 from lbm_amd import cases  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "lib"
-for name in ("ldc256", "c3", "ldc512"):
+names = sys.argv[2].split(",") if len(sys.argv) > 2 else ["ldc256", "c3", "ldc512"]
+for name in names:
     if name == "c3":
         lat, geo = cases.poiseuille(128, 512, 128)
         cells, steps = geo.size, 200
     else:
         n = int(name[3:])
         lat = cases.ldc_device(n, n, n)
-        cells, steps = n ** 3, 200 if n == 256 else 50
+        cells, steps = n ** 3, 200 if n == 256 else int(os.environ.get("LAB_STEPS512", "50"))
     lat.step(20, history=False)
     lat.sync()
     t = time.perf_counter()
