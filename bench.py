@@ -106,6 +106,7 @@ def c5_one_gpu(dev: int, steps: int = 10):
 
 def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
     lay = lat.layout()
+    shape = lat.launch_shape()
     lat.step(warm, history=False)
     lat.sync()
     t = time.perf_counter()
@@ -116,6 +117,8 @@ def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
     out = {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
     out["rows_along"] = "xy"[lay["row_axis"] - 1]
     out["active_chunks"] = lay["active_chunks"]
+    out["cells_per_lane"] = shape["cells_per_lane"]
+    out["grid_stride"] = shape["grid_stride"]
     return out
 
 
@@ -242,6 +245,7 @@ def main():
         every = [mine]
     parity_ms = [round(st[f"step_kernel_src{b}_ms"] / max(1, st[f"step_kernel_src{b}_launches"]), 4) for b in (0, 1)]
     placement = lat.placement()
+    launch_shape = lat.launch_shape()
     lat.close()
 
     # attainable streaming bandwidth of this device, same run (context for roofline.frac:
@@ -316,6 +320,7 @@ def main():
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
         "step_kernel_ms_by_source_buffer": parity_ms,
         "buffer_placement": placement,
+        "launch_shape": launch_shape,
         "residual_last": state["residual"],
     }
     if world > 1:

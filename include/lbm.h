@@ -149,8 +149,8 @@ const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error
 
 /* Process-wide tuning knobs (not a reference interface: A/B measurement and test switches;
  * the defaults are the measured best).  Read when a context is created (ROW_AXIS,
- * CELLS_PER_LANE, EXACT_DIV, FUSED_RESIDUAL, BUFFER_ALLOC).  Returns the previous value, or
- * LBM_ERR_ARG for an unknown knob / value.  Results are bit-identical for every setting. */
+ * CELLS_PER_LANE, EXACT_DIV, FUSED_RESIDUAL, BUFFER_ALLOC, GRID_STRIDE).  Returns the previous
+ * value, or LBM_ERR_ARG for an unknown knob / value.  Results are bit-identical for every setting. */
 typedef enum {
   LBM_TUNE_ROW_AXIS = 0,        /* stands in for lbm_desc.row_axis = 0: 0 choose, 1 x, 2 y */
   LBM_TUNE_CELLS_PER_LANE = 1,  /* step kernel: 0 by size, 1 one cell per lane, 4 four */
@@ -162,7 +162,11 @@ typedef enum {
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
                                    asynchronous RCCL error always aborts promptly. */
-  LBM_TUNE_COUNT = 6
+  LBM_TUNE_GRID_STRIDE = 6,    /* 4-cell step kernel: 0 (default) by sparsity -- 2 blocks per CU
+                                   whose waves loop over their XCD's chunks when the chunks' lanes
+                                   are under 3/4 busy, else one chunk per wave; 1 one chunk per
+                                   wave; B = 2..8 the loop with at most B blocks per CU */
+  LBM_TUNE_COUNT = 7
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 
@@ -254,6 +258,11 @@ int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen
  * 2 = y; pitch = row slots; x_align 1..4; active_chunks = 256-cell chunks k_step launches a
  * wave for (those holding fluid).  Nullable outputs. */
 int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_t* active_chunks);
+/* How the step kernel covers the whole-domain chunks (not a reference interface: diagnostics
+ * for benchmarks and tests): cells_per_lane 1 or 4, main_blocks = its chunk workgroups,
+ * grid_stride 1 when those loop over their XCD's chunks (LBM_TUNE_GRID_STRIDE), lane_fill =
+ * mean share of chunk lanes with a cell to update.  Nullable outputs. */
+int lbm_get_launch_shape(lbm_ctx* ctx, int* cells_per_lane, int* main_blocks, int* grid_stride, double* lane_fill);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (done by the NEE blocks of
  * the step kernel). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);

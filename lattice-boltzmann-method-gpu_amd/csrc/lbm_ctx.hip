@@ -34,7 +34,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -64,6 +64,8 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   double* part = nullptr; // main partials, then fix-up partials
   int npart = 0;
   int main_blocks = 0, nee_blocks = 0, nee_waves = 4;
+  bool stride = false;    // grid-stride chunk loop (LBM_TUNE_GRID_STRIDE)
+  double lane_fill = 1.0; // 4-cell path: mean share of chunk lanes with a cell to update
   bool quarter = false;   // one cell per lane (small ranges)
 };
 }  // namespace
@@ -308,6 +310,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, int srcbuf, hipStream_t st, const
   a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
   a.partial = r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
+  a.chunk_stride = r.stride ? 1 : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
   a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
@@ -445,6 +448,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   if (!r.quarter && r.nchunks && r.chunk0 < 0) {
     std::vector<unsigned long long> lm(chunks.size());
     bool partial = false;
+    int64_t busy = 0;
     for (size_t j = 0; j < chunks.size(); ++j) {
       unsigned long long m = 0;
       const int64_t base = (int64_t)chunks[j] * kChunk;
@@ -454,16 +458,34 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
           const uint8_t v = t[cell];
           if (in(cell) && (v & kClassMask) == kFluid && !(v & kNeedsMac)) m |= 1ull << l;
         }
+      busy += __builtin_popcountll(m);
       m |= (m << 1) | (m >> 1);
       lm[j] = m;
       partial |= m != ~0ull;
     }
+    r.lane_fill = chunks.empty() ? 1.0 : (double)busy / (64.0 * (double)chunks.size());
     if (partial) {
       HIPCK(c, hipMalloc(&r.lane_masks, sizeof(unsigned long long) * lm.size()));
       HIPCK(c, hipMemcpy(r.lane_masks, lm.data(), sizeof(unsigned long long) * lm.size(), hipMemcpyHostToDevice));
     }
   }
   r.main_blocks = main_grid(r.nchunks, r.quarter);
+  // Sparse chunk lists loop: a partly empty chunk is too little work for a wave of its own
+  // (the upsampled bifurcation: +12% with two blocks per CU looping over their XCD's chunks).
+  // Full chunks do not: boxes and the pipe run 10-13% slower that way (lockstep waves,
+  // profiles/r02_grid_stride_ab.log), so they keep one chunk per wave.
+  const int gs = g_tune[LBM_TUNE_GRID_STRIDE];
+  const int per_cu = gs >= 2 ? gs : (gs == 0 && r.lane_masks && r.lane_fill < 0.75) ? 2 : 0;
+  if (!r.quarter && per_cu > 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->d.device) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int cap = (cus * per_cu + 7) / 8 * 8;
+    if (r.main_blocks > cap) {
+      r.main_blocks = cap;
+      r.stride = true;
+    }
+  }
   r.nee_waves = nee_waves_for(r.nslow, contig);
   r.nee_blocks = nee_grid(r.nslow, r.nee_waves);
   r.npart = r.main_blocks + r.nee_blocks;
@@ -594,7 +616,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1433,6 +1455,15 @@ int lbm_get_layout(lbm_ctx* c, int* row_axis, int* pitch, int* x_align, int64_t*
   if (pitch) *pitch = c->L.pitch;
   if (x_align) *x_align = c->L.xshift + 1;
   if (active_chunks) *active_chunks = c->whole.nchunks;
+  return LBM_OK;
+}
+
+int lbm_get_launch_shape(lbm_ctx* c, int* cells_per_lane, int* main_blocks, int* grid_stride, double* lane_fill) {
+  if (!c) return LBM_ERR_ARG;
+  if (cells_per_lane) *cells_per_lane = c->whole.quarter ? 1 : 4;
+  if (main_blocks) *main_blocks = c->whole.main_blocks;
+  if (grid_stride) *grid_stride = c->whole.stride ? 1 : 0;
+  if (lane_fill) *lane_fill = c->whole.lane_fill;
   return LBM_OK;
 }
 

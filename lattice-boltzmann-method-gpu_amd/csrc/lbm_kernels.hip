@@ -655,6 +655,14 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
         acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
+    } else if (a.chunk_stride) {  // grid-stride: XCD (b & 7) takes its eighth of the list in order
+      const int per = (a.nchunks + 7) >> 3;
+      const int lo = (b & 7) * per, hi = min(a.nchunks, lo + per);
+      const int step = (a.main_blocks >> 3) * (kBlock / 64);
+      for (int i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step) {
+        const uint64_t lm = MASK ? a.lane_masks[i] : ~0ull;
+        acc += process_chunk<FAST, SW, MASK>(a, chunk_of(a, i) * kChunk, lane, lm);
+      }
     } else if (idx < a.nchunks) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
       acc = process_chunk<FAST, SW, MASK>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base

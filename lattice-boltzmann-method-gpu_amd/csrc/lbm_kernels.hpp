@@ -67,6 +67,7 @@ struct MainArgs {
                         // lane l (cells 4l .. 4l+3) or a neighbouring lane holds a cell the chunk
                         // wave updates; the other lanes load nothing (sparse lattices)
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
+  int chunk_stride;     // 1: each XCD's chunk waves loop over its eighth of the chunk list
   int quarter;          // 1: one cell per lane, a wave per 64-cell quarter chunk (small lattices)
   int pitch;
   int64_t plane;

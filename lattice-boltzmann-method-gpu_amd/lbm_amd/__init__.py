@@ -33,7 +33,7 @@ LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_BC_PRESSURE = 0, 1, 2
 LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
 # lbm_tune knobs (include/lbm.h lbm_tune_knob)
 (TUNE_ROW_AXIS, TUNE_CELLS_PER_LANE, TUNE_EXACT_DIV, TUNE_FUSED_RESIDUAL, TUNE_BUFFER_ALLOC,
- TUNE_SYNC_TIMEOUT_S) = range(6)
+ TUNE_SYNC_TIMEOUT_S, TUNE_GRID_STRIDE) = range(7)
 
 # reference per-case constants
 LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55
@@ -85,7 +85,7 @@ LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_tune", "lbm_get_nonfinite", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
-    "lbm_get_layout", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
+    "lbm_get_layout", "lbm_get_launch_shape", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
 ]
 HOST_SYMBOLS = [
@@ -183,6 +183,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_checkpoint_load": (C.c_int, [P, C.c_char_p]),
             "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
             "lbm_get_layout": (C.c_int, [P, ip, ip, ip, i64p]),
+            "lbm_get_launch_shape": (C.c_int, [P, ip, ip, ip, C.POINTER(C.c_double)]),
             "lbm_buffer_placement": (C.c_int, [P, f64p, C.c_int, ip, ip]),
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
@@ -537,6 +538,15 @@ class Lattice:
         self._ck(lbm_lib().lbm_get_layout(self.h, C.byref(ra), C.byref(pitch), C.byref(xa), C.byref(nch)),
                  "lbm_get_layout")
         return {"row_axis": ra.value, "pitch": pitch.value, "x_align": xa.value, "active_chunks": nch.value}
+
+    def launch_shape(self):
+        """How the step kernel covers the chunks: cells per lane, chunk workgroups, whether they
+        loop over their XCD's chunks (grid stride), mean share of busy chunk lanes."""
+        cpl, mb, gs, fill = C.c_int(), C.c_int(), C.c_int(), C.c_double()
+        self._ck(lbm_lib().lbm_get_launch_shape(self.h, C.byref(cpl), C.byref(mb), C.byref(gs), C.byref(fill)),
+                 "lbm_get_launch_shape")
+        return {"cells_per_lane": cpl.value, "main_blocks": mb.value, "grid_stride": gs.value,
+                "lane_fill": round(fill.value, 3)}
 
     def numerics(self):
         """(fast_div in use, chunk waves that took the exact division since creation)."""

@@ -96,14 +96,16 @@ def test_tune_knobs_validated(lbm):
     """lbm_tune (host only, no device needed): returns the previous value, rejects unknown
     knobs and out-of-range values with LBM_ERR_ARG, and the defaults are the documented ones."""
     defaults = {lbm.TUNE_ROW_AXIS: 0, lbm.TUNE_CELLS_PER_LANE: 0, lbm.TUNE_EXACT_DIV: 0,
-                lbm.TUNE_FUSED_RESIDUAL: 1, lbm.TUNE_BUFFER_ALLOC: 0, lbm.TUNE_SYNC_TIMEOUT_S: 0}
+                lbm.TUNE_FUSED_RESIDUAL: 1, lbm.TUNE_BUFFER_ALLOC: 0, lbm.TUNE_SYNC_TIMEOUT_S: 0,
+                lbm.TUNE_GRID_STRIDE: 0}
     for knob, dflt in defaults.items():
         assert lbm.tune(knob, dflt) == dflt
     with lbm.tuned(lbm.TUNE_CELLS_PER_LANE, 4):
         assert lbm.tune(lbm.TUNE_CELLS_PER_LANE, 4) == 4
     assert lbm.tune(lbm.TUNE_CELLS_PER_LANE, 0) == 0
     for knob, value in ((-1, 0), (len(defaults), 0), (lbm.TUNE_ROW_AXIS, 3), (lbm.TUNE_CELLS_PER_LANE, 2),
-                        (lbm.TUNE_CELLS_PER_LANE, 3), (lbm.TUNE_EXACT_DIV, -1), (lbm.TUNE_SYNC_TIMEOUT_S, 86401)):
+                        (lbm.TUNE_CELLS_PER_LANE, 3), (lbm.TUNE_EXACT_DIV, -1), (lbm.TUNE_SYNC_TIMEOUT_S, 86401),
+                        (lbm.TUNE_GRID_STRIDE, 9)):
         with pytest.raises(lbm.LbmError, match="unknown knob or value"):
             lbm.tune(knob, value)
     for knob, dflt in defaults.items():  # a rejected call leaves every knob as it was

@@ -127,6 +127,8 @@ def test_bifurcation_upsampled_bitwise(gpu, oracle):
     oracle's geo_pre, and the lattice steps bit for bit like the oracle."""
     from lbm_amd import cases, index_transform
     lat, up = cases.bifurcation_upsampled(4)
+    shape = lat.launch_shape()  # a sparse list: the chunk waves loop (LBM_TUNE_GRID_STRIDE auto)
+    assert shape["cells_per_lane"] == 4 and shape["grid_stride"] == 1 and shape["lane_fill"] < 0.75, shape
     geo = oracle.geo_mask(up.astype(np.int32))
     got = lat.geo()
     assert np.array_equal(got, geo), f"{np.count_nonzero(got != geo)} codes differ"
@@ -145,3 +147,29 @@ def test_bifurcation_upsampled_bitwise(gpu, oracle):
         o.step(s)
         assert_bitwise(lat, o, geo, 2, f"bif x4 +{s}")
     assert o.bad_reads() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["ldc96", "bif_x4"])
+def test_grid_stride_bitwise(gpu, knob, case):
+    """LBM_TUNE_GRID_STRIDE changes only which wave takes which chunk: forced on (2 and 3
+    blocks per CU) a box lattice and forced off the sparse one step bit for bit like the default
+    (the default paths are pinned to the oracle by the tests above and test_gpu_parity.py)."""
+    from lbm_amd import cases
+    knob(gpu.TUNE_CELLS_PER_LANE, 4)
+
+    def run(v):
+        with gpu.tuned(gpu.TUNE_GRID_STRIDE, v):
+            lat = cases.ldc_device(96, 96, 96) if case == "ldc96" else cases.bifurcation_upsampled(4)[0]
+        shape = lat.launch_shape()
+        lat.step(12, history=False)
+        f = lat.f()
+        lat.close()
+        return shape, f
+
+    s0, f0 = run(0)
+    assert s0["grid_stride"] == (1 if case == "bif_x4" else 0), s0
+    for v in (1, 2, 3):
+        s, f = run(v)
+        assert s["grid_stride"] == (0 if v == 1 else 1), (v, s)
+        assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), f"{case} grid_stride={v}"
