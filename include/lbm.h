@@ -165,7 +165,8 @@ typedef enum {
   LBM_TUNE_GRID_STRIDE = 6,    /* 4-cell step kernel: 0 (default) by sparsity -- 2 blocks per CU
                                    whose waves loop over their XCD's chunks when the chunks' lanes
                                    are under 3/4 busy, else one chunk per wave; 1 one chunk per
-                                   wave; B = 2..8 the loop with at most B blocks per CU */
+                                   wave; B = 2..8 the loop with at most B blocks per CU (sparse
+                                   chunk lists only) */
   LBM_TUNE_COUNT = 7
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);

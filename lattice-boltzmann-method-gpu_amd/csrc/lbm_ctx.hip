@@ -464,7 +464,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       partial |= m != ~0ull;
     }
     r.lane_fill = chunks.empty() ? 1.0 : (double)busy / (64.0 * (double)chunks.size());
-    if (partial) {
+    if (partial || g_tune[LBM_TUNE_GRID_STRIDE] >= 2) {  // the loop kernel reads them
       HIPCK(c, hipMalloc(&r.lane_masks, sizeof(unsigned long long) * lm.size()));
       HIPCK(c, hipMemcpy(r.lane_masks, lm.data(), sizeof(unsigned long long) * lm.size(), hipMemcpyHostToDevice));
     }
@@ -476,7 +476,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // profiles/r02_grid_stride_ab.log), so they keep one chunk per wave.
   const int gs = g_tune[LBM_TUNE_GRID_STRIDE];
   const int per_cu = gs >= 2 ? gs : (gs == 0 && r.lane_masks && r.lane_fill < 0.75) ? 2 : 0;
-  if (!r.quarter && per_cu > 0) {
+  if (!r.quarter && r.lane_masks && per_cu > 0) {  // the loop kernel is the lane-mask one
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->d.device) != hipSuccess || cus <= 0)
       cus = 256;

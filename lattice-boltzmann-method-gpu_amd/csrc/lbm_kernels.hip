@@ -624,7 +624,7 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
   return a.chunk0 >= 0 ? (int64_t)a.chunk0 + idx : (int64_t)a.chunks[idx];
 }
 
-template <bool FAST, bool QUARTER, bool SW, bool MASK = false>
+template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false>
 __device__ __forceinline__ void step_body(const MainArgs& a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -655,7 +655,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
         acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
-    } else if (a.chunk_stride) {  // grid-stride: XCD (b & 7) takes its eighth of the list in order
+    } else if constexpr (STRIDE) {  // grid-stride: XCD (b & 7) takes its eighth of the list in order
       const int per = (a.nchunks + 7) >> 3;
       const int lo = (b & 7) * per, hi = min(a.nchunks, lo + per);
       const int step = (a.main_blocks >> 3) * (kBlock / 64);
@@ -680,9 +680,9 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
 
 // 4 cells per lane (big lattices): two waves per SIMD (216-220 VGPRs); MASK: the range has
 // lane masks (sparse chunk lists)
-template <bool FAST, bool SW, bool MASK>
+template <bool FAST, bool SW, bool MASK, bool STRIDE = false>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
-  step_body<FAST, false, SW, MASK>(a);
+  step_body<FAST, false, SW, MASK, STRIDE>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
 template <bool SW>
@@ -1183,10 +1183,12 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
     k = sw ? k_step1<true> : k_step1<false>;
   } else if (a.fast_div) {
-    if (a.lane_masks) k = sw ? k_step<true, true, true> : k_step<true, false, true>;
+    if (a.chunk_stride) k = sw ? k_step<true, true, true, true> : k_step<true, false, true, true>;
+    else if (a.lane_masks) k = sw ? k_step<true, true, true> : k_step<true, false, true>;
     else k = sw ? k_step<true, true, false> : k_step<true, false, false>;
   } else {
-    if (a.lane_masks) k = sw ? k_step<false, true, true> : k_step<false, false, true>;
+    if (a.chunk_stride) k = sw ? k_step<false, true, true, true> : k_step<false, false, true, true>;
+    else if (a.lane_masks) k = sw ? k_step<false, true, true> : k_step<false, false, true>;
     else k = sw ? k_step<false, true, false> : k_step<false, false, false>;
   }
   hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, a);

@@ -68,6 +68,7 @@ struct MainArgs {
                         // wave updates; the other lanes load nothing (sparse lattices)
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
   int chunk_stride;     // 1: each XCD's chunk waves loop over its eighth of the chunk list
+                        // (lane-mask ranges only: k_step<..., MASK, STRIDE>)
   int quarter;          // 1: one cell per lane, a wave per 64-cell quarter chunk (small lattices)
   int pitch;
   int64_t plane;

@@ -150,17 +150,20 @@ def test_bifurcation_upsampled_bitwise(gpu, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["ldc96", "bif_x4"])
+@pytest.mark.parametrize("case", ["pipe", "bif_x4"])
 def test_grid_stride_bitwise(gpu, knob, case):
-    """LBM_TUNE_GRID_STRIDE changes only which wave takes which chunk: forced on (2 and 3
-    blocks per CU) a box lattice and forced off the sparse one step bit for bit like the default
-    (the default paths are pinned to the oracle by the tests above and test_gpu_parity.py)."""
+    """LBM_TUNE_GRID_STRIDE changes only which wave takes which chunk.  A pipe (a sparse chunk
+    list whose lanes are nearly all busy: one chunk per wave by default) with the loop forced on,
+    and the upsampled bifurcation (half-empty chunks: the loop by default) forced off and on,
+    step bit for bit like their defaults.  The defaults are pinned to the oracle by the tests
+    above and by test_gpu_parity.py."""
     from lbm_amd import cases
     knob(gpu.TUNE_CELLS_PER_LANE, 4)
+    knob(gpu.TUNE_ROW_AXIS, 2)  # rows along the pipe: one chunk per (x, z) column, lanes full
 
     def run(v):
         with gpu.tuned(gpu.TUNE_GRID_STRIDE, v):
-            lat = cases.ldc_device(96, 96, 96) if case == "ldc96" else cases.bifurcation_upsampled(4)[0]
+            lat = cases.poiseuille(64, 256, 64)[0] if case == "pipe" else cases.bifurcation_upsampled(4)[0]
         shape = lat.launch_shape()
         lat.step(12, history=False)
         f = lat.f()
@@ -169,7 +172,7 @@ def test_grid_stride_bitwise(gpu, knob, case):
 
     s0, f0 = run(0)
     assert s0["grid_stride"] == (1 if case == "bif_x4" else 0), s0
-    for v in (1, 2, 3):
+    for v in ((1, 2) if case == "pipe" else (1, 2, 3)):
         s, f = run(v)
         assert s["grid_stride"] == (0 if v == 1 else 1), (v, s)
         assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), f"{case} grid_stride={v}"
