@@ -5,6 +5,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+With --gpus N > 1 and no WORLD_SIZE in the environment (no launcher), bench.py launches
+itself: the parent starts N child processes of this script with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, before it imports torch or touches a
+GPU, waits for them and exits with the worst child status.  The children are the ranks.
+
 Workload (weak scaling): the lid-driven cavity of ldc.cu on a 512 x 512 x (512*N) box split
 into N z-slabs of 512^3 cells, one per GPU (N = 8 is BASELINE.json config C5, N = 1 the
 north-star 512^3 single-GPU lattice).  A step is one reference time step over the whole
@@ -25,19 +30,17 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lattice-boltzmann-method-gpu_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
-
-import torch  # noqa: E402  (before liblbm: one shared HIP runtime)
-import torch.distributed as dist  # noqa: E402
-
-import lbm_amd  # noqa: E402
-from lbm_amd import cases  # noqa: E402
-from lbm_amd import dist as ldist  # noqa: E402
+# torch, torch.distributed and lbm_amd are imported by _imports(): after the self-launch
+# decision, so the launching parent never loads a HIP runtime
+torch = dist = lbm_amd = cases = ldist = None
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_CELL = 152    # 19 fp32 loads + 19 fp32 stores per fluid cell update
@@ -178,7 +181,18 @@ def perturbed_mlups(n: int, steps: int, dev: int):
             "avg_kernel_ms": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]), 4)}
 
 
-def main():
+def _imports():
+    """torch (before liblbm: one shared HIP runtime), torch.distributed and lbm_amd."""
+    global torch, dist, lbm_amd, cases, ldist
+    import torch as _torch
+    import torch.distributed as _dist
+    import lbm_amd as _lbm_amd
+    from lbm_amd import cases as _cases
+    from lbm_amd import dist as _ldist
+    torch, dist, lbm_amd, cases, ldist = _torch, _dist, _lbm_amd, _cases, _ldist
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -186,8 +200,92 @@ def main():
     ap.add_argument("--n", type=int, default=512, help="per-GPU slab edge (nx = ny = nz_local)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int, argv, grace_s: float = 420.0, script=None) -> int:
+    """--gpus n > 1 without a launcher: start n ranks of this script as child processes (the
+    torchrun environment: RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR,
+    MASTER_PORT), wait, return the worst exit status.  Called before torch is imported; the
+    parent never execs.  When a rank fails, the others get `grace_s` seconds to fail too
+    (their RCCL waits give up after LBM_TUNE_SYNC_TIMEOUT_S = 300 s) before they are killed."""
+    port = _free_port()
+    script = script or os.path.abspath(__file__)
+    kids = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        kids.append(subprocess.Popen([sys.executable, script, *argv], env=env))
+    first_fail = None
+    while True:
+        codes = [p.poll() for p in kids]
+        if all(c is not None for c in codes):
+            break
+        if first_fail is None and any(c not in (None, 0) for c in codes):
+            first_fail = time.monotonic()
+        if first_fail is not None and time.monotonic() - first_fail > grace_s:
+            for p in kids:
+                if p.poll() is None:
+                    p.kill()
+            for p in kids:
+                p.wait()
+            break
+        time.sleep(0.2)
+    worst = 0
+    for p in kids:
+        rc = p.returncode
+        rc = 128 - rc if rc < 0 else rc  # killed by signal s: 128 + s, as a shell reports it
+        if rc and (worst == 0 or rc > worst):
+            worst = rc
+    return worst
+
+
+def check_rccl_ranks(rank: int, rccl_ranks: int, world: int):
+    """The communicator liblbm built must span every rank (ncclCommCount)."""
+    if rccl_ranks != world:
+        raise SystemExit(f"rank {rank}: RCCL communicator has {rccl_ranks} ranks, WORLD_SIZE {world}")
+
+
+def gather_ranks(mine, elapsed: float, kern_ms: float, main_ms: float, n_fluid: int, world: int, group=None):
+    """N > 1: the slowest rank's wall time and kernel times (max over ranks), the fluid cells of
+    all slabs (sum) and every rank's row `mine` = [rank, rccl_ranks, edge, interior, halo,
+    halo_exposed, wall] (ms per step), gathered over torch.distributed (gloo)."""
+    elapsed, kern_ms, main_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms], group)
+    n_fluid_total = int(ldist.sum_over_ranks([n_fluid], group)[0])
+    every = [None] * world
+    dist.all_gather_object(every, list(mine), group=group)
+    return elapsed, kern_ms, main_ms, n_fluid_total, every
+
+
+def multi_gpu_block(every) -> dict:
+    """The N > 1 bench line's `multi_gpu` object from the gathered per-rank rows: per-rank slab
+    timings (HIP events, ms per step) -- edge-plane launch, interior launch, halo exchange on the
+    communication stream, and the part of the halo that outlasted the interior launch (not
+    hidden) -- the smallest communicator any rank saw, and the hidden share of the halo."""
+    ranks = [{"rank": int(r[0]), "rccl_ranks": int(r[1]), "edge_ms": round(r[2], 4), "interior_ms": round(r[3], 4),
+              "halo_ms": round(r[4], 4), "halo_exposed_ms": round(r[5], 4), "wall_ms_per_step": round(r[6], 4)}
+             for r in sorted(every)]
+    halo = sum(r["halo_ms"] for r in ranks)
+    return {
+        "rccl_ranks": min(r["rccl_ranks"] for r in ranks),
+        "halo_hidden_frac": round(1.0 - sum(r["halo_exposed_ms"] for r in ranks) / halo, 4) if halo > 0 else None,
+        "per_rank": ranks,
+    }
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    _imports()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -208,8 +306,7 @@ def main():
         lbm_amd.tune(lbm_amd.TUNE_SYNC_TIMEOUT_S, 300)
         lat.attach_rccl(ldist.share_unique_id(rank, None, lbm_amd.rccl_unique_id), rank, world)
     rccl_rank, rccl_ranks = lat.comm_info()
-    if rccl_ranks != world:
-        raise SystemExit(f"rank {rank}: RCCL communicator has {rccl_ranks} ranks, WORLD_SIZE {world}")
+    check_rccl_ranks(rank, rccl_ranks, world)
     counts = lat.counts()
 
     def barrier():
@@ -236,10 +333,8 @@ def main():
     mine = [rank, rccl_ranks, per_step("edge"), per_step("interior"), per_step("halo"), per_step("halo_exposed"),
             elapsed / args.steps * 1e3]
     if world > 1:
-        elapsed, kern_ms, main_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms], None)
-        n_fluid_total = int(ldist.sum_over_ranks([counts["n_fluid"]], None)[0])
-        every = [None] * world
-        dist.all_gather_object(every, mine)
+        elapsed, kern_ms, main_ms, n_fluid_total, every = gather_ranks(mine, elapsed, kern_ms, main_ms,
+                                                                      counts["n_fluid"], world)
     else:
         n_fluid_total = counts["n_fluid"]
         every = [mine]
@@ -324,18 +419,7 @@ def main():
         "residual_last": state["residual"],
     }
     if world > 1:
-        # per-rank slab timings (HIP events, ms per step): edge-plane launch, interior launch,
-        # halo exchange on the communication stream, and the part of the halo that outlasted
-        # the interior launch (not hidden)
-        ranks = [{"rank": r[0], "rccl_ranks": r[1], "edge_ms": round(r[2], 4), "interior_ms": round(r[3], 4),
-                  "halo_ms": round(r[4], 4), "halo_exposed_ms": round(r[5], 4), "wall_ms_per_step": round(r[6], 4)}
-                 for r in sorted(every)]
-        halo = sum(r["halo_ms"] for r in ranks)
-        line["multi_gpu"] = {
-            "rccl_ranks": min(r["rccl_ranks"] for r in ranks),
-            "halo_hidden_frac": round(1.0 - sum(r["halo_exposed_ms"] for r in ranks) / halo, 4) if halo > 0 else None,
-            "per_rank": ranks,
-        }
+        line["multi_gpu"] = multi_gpu_block(every)
     if world == 1 and not args.no_secondary:
         line["secondary"] = {"ldc64_mlups (published config)": small_case_mlups(64, 2000, local),
                              "ldc256_mlups (config C2)": small_case_mlups(256, 200, local),

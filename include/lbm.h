@@ -150,7 +150,10 @@ const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error
 /* Process-wide tuning knobs (not a reference interface: A/B measurement and test switches;
  * the defaults are the measured best).  Read when a context is created (ROW_AXIS,
  * CELLS_PER_LANE, EXACT_DIV, FUSED_RESIDUAL, BUFFER_ALLOC, GRID_STRIDE).  Returns the previous
- * value, or LBM_ERR_ARG for an unknown knob / value.  Results are bit-identical for every setting. */
+ * value, or LBM_ERR_ARG for an unknown knob / value.  Fields (populations, rho, u) are
+ * bit-identical for every setting; the residual's fp64 |u| sum is accumulated per launch block,
+ * so launch-shape knobs (CELLS_PER_LANE, GRID_STRIDE, FUSED_RESIDUAL) can change its last bits
+ * and with them, rarely, the step a convergence-controlled run stops at. */
 typedef enum {
   LBM_TUNE_ROW_AXIS = 0,        /* stands in for lbm_desc.row_axis = 0: 0 choose, 1 x, 2 y */
   LBM_TUNE_CELLS_PER_LANE = 1,  /* step kernel: 0 by size, 1 one cell per lane, 4 four */
@@ -167,7 +170,10 @@ typedef enum {
                                    are under 3/4 busy, else one chunk per wave; 1 one chunk per
                                    wave; B = 2..8 the loop with at most B blocks per CU (sparse
                                    chunk lists only) */
-  LBM_TUNE_COUNT = 7
+  LBM_TUNE_INJECT_RCCL_FAULT = 7, /* test hook: 1 = the next wait of an RCCL context (lbm_sync, a
+                                   synchronising lbm_step, a read-out) sees a failed peer; the knob
+                                   resets itself.  Exercises the abort path below. */
+  LBM_TUNE_COUNT = 8
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 
@@ -242,8 +248,8 @@ int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_b
 int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
 /* Arithmetic of the relaxation's division by tau (the reference divides, ldc.cu:326-363):
  * fast_div = 1 when the 3-instruction correctly rounded quotient is in use (tau verified
- * exhaustively at lbm_create; LBM_EXACT_DIV=1 in the environment forces the compiler's
- * division).  A wave whose populations leave the quotient's proven domain (|f| outside
+ * exhaustively at lbm_create; lbm_tune(LBM_TUNE_EXACT_DIV, 1) before lbm_create forces the
+ * compiler's division).  A wave whose populations leave the quotient's proven domain (|f| outside
  * [2^-60, 2^40) or |u| >= 2^10, e.g. a diverging run) relaxes with the exact division
  * instead (a wave-uniform branch in the same launch); retried_chunks counts those 256-cell
  * chunk waves since creation.  Results are bit-identical either way. */
@@ -289,7 +295,10 @@ int lbm_probe_stream_shapes(int device, int64_t bytes, int reps, double* gbs_sha
  * residual sum. */
 int lbm_rccl_unique_id(uint8_t out_id[128]);
 int lbm_attach_rccl(lbm_ctx* ctx, const uint8_t id[128], int rank, int nranks);
-/* rank and communicator size as RCCL reports them (ncclCommCount); 0 / 1 without RCCL. */
+/* rank and communicator size as RCCL reports them (ncclCommCount); 0 / 1 without RCCL.
+ * A communicator aborted by a failed peer or a timed-out wait stays failed: from then on
+ * lbm_step, lbm_sync, every read-out, lbm_checkpoint_save and lbm_comm_info return
+ * LBM_ERR_RCCL (the slab's ghost planes and residual are stale); destroy the context. */
 int lbm_comm_info(lbm_ctx* ctx, int* rank, int* nranks);
 
 /* Single-device loopback decomposition (test and debug path): n contexts, each a z-slab of

@@ -34,7 +34,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -125,6 +125,10 @@ struct lbm_ctx {
   // rccl
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  // sticky: the communicator was aborted (a peer failed or a wait timed out).  The ghost planes
+  // and the residual are stale from then on, so every later step, wait and read-out fails with
+  // LBM_ERR_RCCL instead of silently running the slab as a single domain
+  bool comm_failed = false;
   std::string err;
 };
 
@@ -616,7 +620,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 1};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1123,7 +1127,14 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
 // peer that failed (ncclCommGetAsyncError) or a wait longer than LBM_TUNE_SYNC_TIMEOUT_S
 // aborts the communicator and returns LBM_ERR_RCCL, so a rank whose neighbour died exits
 // promptly instead of hanging in a halo receive.
+int comm_failed_error(lbm_ctx* c) {
+  c->err = "RCCL communicator was aborted after a peer failure or a timed-out wait; the slab state is stale "
+           "(destroy the context)";
+  return LBM_ERR_RCCL;
+}
+
 int wait_streams(lbm_ctx* c) {
+  if (c->comm_failed) return comm_failed_error(c);
   if (!c->comm) {
     HIPCK(c, hipStreamSynchronize(c->s_comp));
     HIPCK(c, hipStreamSynchronize(c->s_comm));
@@ -1132,12 +1143,17 @@ int wait_streams(lbm_ctx* c) {
   const auto t0 = std::chrono::steady_clock::now();
   const int limit_s = g_tune[LBM_TUNE_SYNC_TIMEOUT_S];
   for (;;) {
-    const hipError_t a = hipStreamQuery(c->s_comp), b = hipStreamQuery(c->s_comm);
-    if (a == hipSuccess && b == hipSuccess) return LBM_OK;
-    if (a != hipSuccess && a != hipErrorNotReady) HIPCK(c, a);
-    if (b != hipSuccess && b != hipErrorNotReady) HIPCK(c, b);
     ncclResult_t ar = ncclSuccess;
-    NCCK(c, ncclCommGetAsyncError(c->comm, &ar));
+    if (g_tune[LBM_TUNE_INJECT_RCCL_FAULT]) {  // test hook: this wait sees a failed peer
+      g_tune[LBM_TUNE_INJECT_RCCL_FAULT] = 0;
+      ar = ncclRemoteError;
+    } else {
+      const hipError_t a = hipStreamQuery(c->s_comp), b = hipStreamQuery(c->s_comm);
+      if (a == hipSuccess && b == hipSuccess) return LBM_OK;
+      if (a != hipSuccess && a != hipErrorNotReady) HIPCK(c, a);
+      if (b != hipSuccess && b != hipErrorNotReady) HIPCK(c, b);
+      NCCK(c, ncclCommGetAsyncError(c->comm, &ar));
+    }
     const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if ((ar != ncclSuccess && ar != ncclInProgress) || (limit_s > 0 && waited > limit_s)) {
       c->err = ar != ncclSuccess && ar != ncclInProgress
@@ -1145,6 +1161,7 @@ int wait_streams(lbm_ctx* c) {
                    : "RCCL step did not complete within LBM_TUNE_SYNC_TIMEOUT_S = " + std::to_string(limit_s) + " s";
       (void)ncclCommAbort(c->comm);
       c->comm = nullptr;
+      c->comm_failed = true;
       return LBM_ERR_RCCL;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(waited < 0.01 ? 20 : 200));
@@ -1180,6 +1197,7 @@ extern "C" {
 
 int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
   if (!c || nsteps < 0) return LBM_ERR_ARG;
+  if (c->comm_failed) return comm_failed_error(c);
   if (nsteps == 0) {
     if (steps_done) *steps_done = c->steps_done;
     return LBM_OK;
@@ -1402,6 +1420,16 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
                h.pitch == c->L.pitch && h.xshift == c->L.xshift && h.tau_bits == tau_bits &&
                h.ncell == c->L.ncell && h.buf_floats == c->L.nchunk * kQ * kChunk;
   for (int i = 0; i < 3 && match; ++i) match = h.nslow[i] == rs[i]->nslow;
+  // run state of a well-formed file: one of the two buffers current, flags 0/1, the device
+  // step counter equal to the host's
+  const bool sane = (h.cur == 0 || h.cur == 1) && h.steps_done >= 0 && (h.last_slab == 0 || h.last_slab == 1) &&
+                    (h.halo_primed == 0 || h.halo_primed == 1) && h.conv.k == h.steps_done &&
+                    h.conv.tol_count >= 0 && h.conv.stopped >= 0 && h.conv.stopped <= 2;
+  if (match && !sane) {
+    std::fclose(f);
+    c->err = std::string("lbm_checkpoint_load: ") + path + ": corrupt header (buffer index, step or flags)";
+    return LBM_ERR_ARG;
+  }
   if (!match) {
     std::fclose(f);
     c->err = std::string("lbm_checkpoint_load: ") + path +
@@ -1429,7 +1457,19 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
     c->err = std::string("lbm_checkpoint_load: truncated file ") + path;
     return LBM_ERR_ARG;
   }
-  HIPCK(c, hipMemcpy(c->conv, &h.conv, sizeof(ConvState), hipMemcpyHostToDevice));
+  {
+    // the run state comes from the file; the convergence settings (enabled, max_it, stag_max,
+    // tol) stay this context's own, which the step kernels' stop flag follows (conv_enabled)
+    ConvState now{};
+    HIPCK(c, hipMemcpy(&now, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
+    ConvState run = h.conv;
+    run.enabled = now.enabled;
+    run.max_it = now.max_it;
+    run.stag_max = now.stag_max;
+    run.tol = now.tol;
+    if (!run.enabled) run.stopped = 0;  // as lbm_set_convergence(0, ...) leaves it
+    HIPCK(c, hipMemcpy(c->conv, &run, sizeof(ConvState), hipMemcpyHostToDevice));
+  }
   c->cur = h.cur;
   c->steps_done = h.steps_done;
   c->macros_stale = h.steps_done > 0;
@@ -1612,6 +1652,7 @@ int lbm_rccl_unique_id(uint8_t out_id[128]) {
 
 int lbm_comm_info(lbm_ctx* c, int* rank, int* nranks) {
   if (!c) return LBM_ERR_ARG;
+  if (c->comm_failed) return comm_failed_error(c);
   int n = 1;
   if (c->comm) NCCK(c, ncclCommCount(c->comm, &n));
   if (rank) *rank = c->comm ? c->rank : 0;

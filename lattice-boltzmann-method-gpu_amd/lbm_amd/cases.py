@@ -178,9 +178,9 @@ def coronary_bc_codes(c_u: float = 2.74909090909091):
     code 2 inlet (fluid at x+1): u_bc = (0.1745/C_U, 0, 0), rho_bc = 1;
     code 3 outlet (fluid at x-1): u_bc = (0.1/C_U, 0, 0), rho of the fluid neighbour;
     codes 5, 6, 7 outlets (fluid at z-1): u_bc = (0, 0, 0.02/C_U), rho of the fluid neighbour.
-    The velocities are the reference's double quotients rounded to float.  (The reference's
-    code-3 branch writes its q = 10 value into slot 14 with q = 9's operands -- a slip this
-    table does not copy: every outgoing q gets its own NEE value.)"""
+    The velocities are the reference's double quotients rounded to float.  Each outgoing
+    population gets its own NEE value from its own fluid neighbour and equilibrium (the code-3
+    branch, coronary.cu:795-867, writes slots 2, 9, 10, 13 and 14 that way)."""
     from . import LBM_BC_VELOCITY, LBM_BC_VELOCITY_RHO, LBM_FACE_NX, LBM_FACE_NZ, LBM_FACE_PX
     cu = np.float32(c_u)
     uin = float(np.float32(0.1745 / float(cu)))

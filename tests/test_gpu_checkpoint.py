@@ -157,3 +157,56 @@ def test_resume_rccl_slab(gpu, tmp_path):
     _same(a.macros(), b.macros(), "RCCL slab macros")
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("saved_on", [True, False])
+def test_load_keeps_this_contexts_convergence_settings(gpu, tmp_path, saved_on):
+    """The file supplies the run state (k, tol_count, residual, sums, stop flag); the
+    convergence settings stay the loading context's own, and its step kernels follow them: a
+    checkpoint saved with convergence control on loads into a context without it and keeps
+    stepping (and the reverse stops at the loading context's max_it)."""
+    from lbm_amd import cases
+    a = cases.ldc(20)[0]
+    if saved_on:
+        a.set_convergence(True, max_it=12, stag_max=50, tol=1e-6)
+    a.step(10)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    b = cases.ldc(20)[0]
+    if not saved_on:
+        b.set_convergence(True, max_it=12, stag_max=50, tol=1e-6)
+    b.checkpoint_load(path)
+    b.step(20)
+    st = b.state()
+    if saved_on:   # b has no convergence control: all 20 steps run
+        assert st["k"] == 30 and st["stopped"] == 0, st
+    else:          # b stops once k > max_it = 12
+        assert st["k"] == 13 and st["stopped"] == 1, st
+    a.close()
+    b.close()
+
+
+def test_load_rejects_corrupt_header(gpu, tmp_path):
+    """A header whose run state is out of range (buffer index, step count, flags) is refused
+    with LBM_ERR_ARG before anything is copied to the device."""
+    import struct
+    from lbm_amd import cases, LbmError
+    a = cases.ldc(16)[0]
+    a.step(3)
+    path = tmp_path / "ck.bin"
+    a.checkpoint_save(str(path))
+    raw = bytearray(path.read_bytes())
+    # CkptHeader: magic[8], then int32 version, nx, ny, nz, z_offset, nz_global, case_kind, swap,
+    # pitch, xshift, steps_done, cur, ...
+    cur_at = 8 + 4 * 11
+    assert struct.unpack_from("<i", raw, cur_at)[0] in (0, 1)
+    for at, val in ((cur_at, 7), (cur_at - 4, -2), (cur_at - 4, 4)):  # cur, steps_done < 0, k != steps_done
+        bad = bytearray(raw)
+        struct.pack_into("<i", bad, at, val)
+        p = tmp_path / f"bad{at}_{val}.bin"
+        p.write_bytes(bytes(bad))
+        b = cases.ldc(16)[0]
+        with pytest.raises(LbmError, match="corrupt header"):
+            b.checkpoint_load(str(p))
+        b.close()
+    a.close()

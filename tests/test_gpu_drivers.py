@@ -164,7 +164,14 @@ def test_bifurcation_driver(gpu, oracle, tmp_path, block):
         got = (tmp_path / "out" / f"bif_{k}.vtk").read_text()
         assert got == _vtk_mask_independent(None, geo, ux, uy, uz, C_U, CH), f"bif_{k}.vtk"
         s1, s2 = _calc_res_ld(geo, *prev), _calc_res_ld(geo, ux, uy, uz)
-        residuals.append(np.float32(abs(s1 - s2) / s2))
+        if s2 == 0:
+            # bifurcation.cu:1269 divides 0 by 0 when both sums vanish (the as-shipped inlet at
+            # step 0): x86 yields the default NaN, printed "-nan" -- expected only in that case
+            assert s1 == 0, (k, s1)
+            residuals.append(-np.float32(np.nan))
+        else:
+            residuals.append(np.float32(abs(s1 - s2) / s2))
+            assert np.isfinite(residuals[-1]), (k, s1, s2)
         prev = (ux, uy, uz)
     log = (tmp_path / "out" / "CONVERGENCE.log").read_text().strip().splitlines()
     assert log[:2] == [_cfmt(r) for r in residuals]

@@ -165,14 +165,17 @@ def test_grid_stride_bitwise(gpu, knob, case):
         with gpu.tuned(gpu.TUNE_GRID_STRIDE, v):
             lat = cases.poiseuille(64, 256, 64)[0] if case == "pipe" else cases.bifurcation_upsampled(4)[0]
         shape = lat.launch_shape()
-        lat.step(12, history=False)
+        hist = lat.step(12)
         f = lat.f()
         lat.close()
-        return shape, f
+        return shape, f, hist
 
-    s0, f0 = run(0)
+    s0, f0, h0 = run(0)
     assert s0["grid_stride"] == (1 if case == "bif_x4" else 0), s0
     for v in ((1, 2) if case == "pipe" else (1, 2, 3)):
-        s, f = run(v)
+        s, f, h = run(v)
         assert s["grid_stride"] == (0 if v == 1 else 1), (v, s)
         assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), f"{case} grid_stride={v}"
+        # the residual's fp64 |u| sum is accumulated per block, so the launch shape may move its
+        # last bits: the fp32 sums S_k agree to an ulp, the residuals to ~1e-7 absolute (lbm.h)
+        assert np.all(np.isfinite(h)) and np.allclose(h, h0, rtol=0, atol=2e-7), (v, h, h0)

@@ -468,3 +468,26 @@ def test_north_star_512_bitwise(gpu, oracle):
     assert abs(velsum - s64) <= 1e-12 * s64, (velsum, s64)
     assert np.all(np.isfinite(hg))
     np.testing.assert_allclose(hg, ho, rtol=0, atol=5e-3)
+
+
+def test_rccl_abort_is_sticky(gpu, knob):
+    """A wait that sees a failed peer aborts the communicator (here injected with
+    LBM_TUNE_INJECT_RCCL_FAULT on a one-rank RCCL slab).  From then on the context refuses to
+    step, wait, read out or checkpoint with LBM_ERR_RCCL -- it does not fall back to stepping
+    the slab as a single domain with stale ghost planes."""
+    from lbm_amd import cases, LbmError
+    import lbm_amd
+    lat = cases.ldc_device(24, 24, 24)
+    lat.attach_rccl(lbm_amd.rccl_unique_id(), 0, 1)
+    lat.step(3)
+    lat.step(2, history=False)
+    lat.sync()  # streams drained: the abort below finds no work in flight
+    knob(lbm_amd.TUNE_INJECT_RCCL_FAULT, 1)
+    with pytest.raises(LbmError, match="RCCL peer failure"):
+        lat.sync()
+    assert lbm_amd.tune(lbm_amd.TUNE_INJECT_RCCL_FAULT, 0) == 0  # the hook fired once and reset
+    for call in (lambda: lat.step(1), lat.sync, lat.macros, lat.state, lat.comm_info, lat.f,
+                 lambda: lat.checkpoint_save("/tmp/never_written.bin")):
+        with pytest.raises(LbmError, match="aborted"):
+            call()
+    lat.close()
