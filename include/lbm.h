@@ -62,7 +62,9 @@ typedef enum { LBM_FACE_PX = 0, LBM_FACE_NX = 1, LBM_FACE_PY = 2, LBM_FACE_NY = 
                LBM_FACE_NZ = 5 } lbm_face;
 
 /* Non-equilibrium extrapolation: f_q(B) = feq_q(rho_bc, u_bc) + (f_q(F) - feq_q(rho_F, u_F)) (1 - 1/tau)
- * with F the fluid neighbour and its previous-step macros. */
+ * with F = B + e_q the fluid neighbour, its post-collision f_q and its (rho, u) of the same step
+ * (boundary_stream, ldc.cu:391-456).  F -- the only cell that pulls slot q of B -- stores the
+ * value itself right after its collision. */
 typedef enum {
   LBM_BC_VELOCITY = 0,      /* u_bc given, rho_bc = rho_F (LDC lid, Poiseuille, bifurcation inlet,
                                coronary outlets coronary.cu:795-943) */
@@ -82,10 +84,8 @@ typedef struct {
   const float* u_normal_table;
 } lbm_bc_code;
 /* Boundary data are static for a context's lifetime: the (rho_bc, u_bc) of every NEE cell --
- * lid speed, inlet/outlet tables, bc_codes -- is fixed by lbm_create and the lbm_init_* call,
- * and each NEE-adjacent fluid cell's work list gathers its boundary neighbours' data once, when
- * the lists are built.  No entry point changes them later; one that did would have to rebuild
- * (re-gather) those lists as well. */
+ * lid speed, inlet/outlet tables, bc_codes -- is fixed by lbm_create.  No entry point changes
+ * them later. */
 
 /* Equilibrium expression used to initialise f (the two forms of the reference). */
 typedef enum {
@@ -134,8 +134,8 @@ typedef struct {
 } lbm_desc;
 
 /* Checkpoint / resume (not in the reference, whose VTK output cannot restart a run; SURVEY.md
- * section 5): the context's complete state -- both population buffers in the device layout, the
- * NEE-adjacent cells' previous (rho, u), the step count and the convergence state -- to a file,
+ * section 5): the context's complete state -- both population buffers in the device layout
+ * (NEE values included), the step count and the convergence state -- to a file,
  * and back into a context created with the same descriptor (extent, slab, case, tau and
  * layout are checked; LBM_ERR_ARG otherwise).  A resumed run continues bit for bit.  Slab
  * contexts save and load one file per rank (ghost planes included).
@@ -240,7 +240,7 @@ int lbm_get_counts(lbm_ctx* ctx, int64_t* n_box, int64_t* n_fluid, double* algo_
 int lbm_profile(lbm_ctx* ctx, int enabled);
 int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
 /* The same for one kind of launch: kind 0 = the step kernel (k_step: stream-collide with
- * bounce-back and the NEE-adjacent cells, one launch per step and launch range); kinds 1 / 2 =
+ * bounce-back and NEE values stored producer-side, one launch per step and launch range); kinds 1 / 2 =
  * those of its launches that read population buffer 0 / 1 (the A-B parity); slabs with RCCL:
  * 3 = the edge-plane launches, 4 = the interior launches, 5 = the halo exchange on the
  * communication stream (pack, send/recv, unpack), 6 = how long each step's halo outlasted its
@@ -270,8 +270,8 @@ int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_
  * grid_stride 1 when those loop over their XCD's chunks (LBM_TUNE_GRID_STRIDE), lane_fill =
  * mean share of chunk lanes with a cell to update.  Nullable outputs. */
 int lbm_get_launch_shape(lbm_ctx* ctx, int* cells_per_lane, int* main_blocks, int* grid_stride, double* lane_fill);
-/* Fluid cells next to a non-equilibrium-extrapolation boundary (done by the NEE blocks of
- * the step kernel). */
+/* Fluid cells next to a non-equilibrium-extrapolation boundary (each stores its NEE
+ * neighbours' values, producer side). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
 
 /* Measurement helper (not a reference interface): the HBM rate a plain streaming copy

@@ -3,13 +3,14 @@
 // A context owns one lattice (or one z-slab of it) on one device:
 //   two AoSoA population buffers (A-B pattern; the reference's d_scr/d_dst, ldc.cu:640-641),
 //   the cell-type bytes (the reference's d_geo + texture-bound index, Poiseulle.cu:49-50),
-//   (rho, u) arrays (d_rho/d_ux/d_uy/d_uz), per-cell wall-link masks, per launch-range work
-//   lists (active 256-cell chunks, NEE-adjacent cells), block partials of the |u| sum and the device-resident
-//   state of the reference main loop (ldc.cu:613-685).
+//   (rho, u) arrays (d_rho/d_ux/d_uy/d_uz; NEE cells hold their boundary data there), per-cell
+//   wall- and NEE-link masks, per launch-range work lists (active 256-cell chunks), block
+//   partials of the |u| sum and the device-resident state of the reference main loop
+//   (ldc.cu:613-685).
 // The reference's per-step sequence update -> boundary_stream -> calc_vel_square ->
-// thrust::reduce -> host residual (ldc.cu:654-684) becomes k_stream_collide +
-// k_boundary_fixup + a two-level deterministic reduction, with no host synchronisation
-// inside a call.  Slabs exchange the 5 populations crossing each +-z face (packed) over
+// thrust::reduce -> host residual (ldc.cu:654-684) becomes one k_step launch (boundary values
+// stored producer-side) + a deterministic reduction folded into the next launch, with no host
+// synchronisation inside a call.  Slabs exchange the 5 populations crossing each +-z face (packed) over
 // RCCL on a second stream while the interior updates.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -55,15 +56,10 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int* chunks = nullptr;  // active 256-cell chunks (>= 1 fluid cell in range)
   int chunk0 = -1;        // >= 0: chunks is chunk0, chunk0 + 1, ... (the kernel skips the list)
   int nchunks = 0;
-  int* cells = nullptr;   // NEE-adjacent fluid cells
-  int nslow = 0;
-  float4* prev = nullptr; // their (rho, u) of the previous step
-  uint2* nee_mask = nullptr;  // their NEE-supplied / pressure directions (static geometry)
-  float4* nee_bc = nullptr;   // their first kNeeSlots NEE neighbours' boundary data (static)
   unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
-  double* part = nullptr; // main partials, then fix-up partials
+  double* part = nullptr; // one |u| partial per chunk block
   int npart = 0;
-  int main_blocks = 0, nee_blocks = 0, nee_waves = 4;
+  int main_blocks = 0;
   bool stride = false;    // grid-stride chunk loop (LBM_TUNE_GRID_STRIDE)
   double lane_fill = 1.0; // 4-cell path: mean share of chunk lanes with a cell to update
   bool quarter = false;   // one cell per lane (small ranges)
@@ -81,7 +77,8 @@ struct lbm_ctx {
   float* buf[2] = {nullptr, nullptr};  // past the guard chunk
   int cur = 0;                         // buf[cur] holds the current state (every launch flips it)
   uint8_t* type = nullptr;
-  uint32_t* links = nullptr;
+  uint32_t* links = nullptr;   // wall-link masks
+  uint32_t* nlinks = nullptr;  // NEE-link masks
   int8_t* codes = nullptr;               // reference codes per storage cell (lbm_get_geo)
   float *bc_in = nullptr, *bc_out = nullptr;  // inlet / outlet u_y tables (lbm_init_case)
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
@@ -121,7 +118,6 @@ struct lbm_ctx {
   // lazy macros (k_moments): the step kernels store none; lbm_get_macros recomputes them
   // from the last step's source buffer when macros_stale
   bool macros_stale = false;
-  bool last_slab = false;  // the last steps ran the slab ranges (edge + mid), not whole
   // rccl
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -292,7 +288,7 @@ struct FusedRed {
 void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
   a.src = c->buf[srcbuf];
   a.dst = c->buf[srcbuf ^ 1];
-  a.type = c->type; a.links = c->links;
+  a.type = c->type; a.links = c->links; a.nlinks = c->nlinks;
   a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
   a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.tau = c->tau;
@@ -303,32 +299,17 @@ void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
   a.swap = c->L.swap;
 }
 
-// one step of a range from buffer srcbuf into srcbuf ^ 1 (hstep: the step's number, for the
-// raw NEE pulls of step 0)
-int run_range(lbm_ctx* c, Range& r, int hstep, int srcbuf, hipStream_t st, const FusedRed* fr = nullptr,
-              int range_kind = -1) {
+// one step of a range from buffer srcbuf into srcbuf ^ 1
+int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* fr = nullptr, int range_kind = -1) {
   MainArgs a{};
-  a.src = c->buf[srcbuf];
-  a.dst = c->buf[srcbuf ^ 1];
-  a.type = c->type; a.links = c->links;
-  a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
+  fill_main_args(c, a, srcbuf);
   a.partial = r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
-  a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
-  a.tau = c->tau;
-  a.tau_rcp = 1.0f / c->tau;
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
-  a.tau_fast = c->fast_div ? 1 : 0;
-  a.exact_waves = c->retried;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
-  a.cells = r.cells; a.prev = r.prev; a.nee_mask = r.nee_mask; a.nee_bc = r.nee_bc; a.n_nee = r.nslow; a.nee_blocks = r.nee_blocks;
-  a.nee_waves = r.nee_waves;
-  a.nee_active = hstep == 0 ? 0 : 1;
-  a.omc = c->omc;
-  a.swap = c->L.swap;
   if (fr) {
     a.partial = fr->part;
     a.red_blocks = 8;
@@ -337,7 +318,7 @@ int run_range(lbm_ctx* c, Range& r, int hstep, int srcbuf, hipStream_t st, const
     a.red_conv = c->conv;
     a.red_hist = fr->hist;
   }
-  if (r.main_blocks + r.nee_blocks > 0 || fr) {
+  if (r.main_blocks > 0 || fr) {
     c->launches++;
     RCK(timed(c, st, kKindStep, kKindSrc0 + srcbuf, range_kind, [&] {
                 HIPCK(c, launch_step(a, st));
@@ -356,7 +337,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   r.c_hi = hi;
   r.c_lo2 = lo2;
   r.c_hi2 = hi2;
-  std::vector<int> chunks, cells;
+  std::vector<int> chunks;
   auto in = [&](int64_t k) { return (k >= lo && k < hi) || (k >= lo2 && k < hi2); };
   auto scan = [&](int64_t a, int64_t b) {
     for (int64_t ch = a / kChunk; ch * kChunk < b; ++ch) {
@@ -367,84 +348,26 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         const uint8_t v = t[k];
         if ((v & kClassMask) != kFluid) continue;
         any = true;
-        if (v & kNeedsMac) cells.push_back((int)k);
       }
       if (any) chunks.push_back((int)ch);
     }
   };
   scan(lo, hi);
   if (hi2 > lo2) scan(lo2, hi2);
-  double contig = 1.0;
   r.nchunks = (int)chunks.size();
   r.chunk0 = chunks.empty() ? -1 : chunks[0];
   for (size_t i = 1; i < chunks.size() && r.chunk0 >= 0; ++i)
     if (chunks[i] != chunks[0] + (int)i) r.chunk0 = -1;
-  r.nslow = (int)cells.size();
   if (r.nchunks) {
     HIPCK(c, hipMalloc(&r.chunks, sizeof(int) * r.nchunks));
     HIPCK(c, hipMemcpy(r.chunks, chunks.data(), sizeof(int) * r.nchunks, hipMemcpyHostToDevice));
-  }
-  if (r.nslow) {
-    HIPCK(c, hipMalloc(&r.cells, sizeof(int) * r.nslow));
-    HIPCK(c, hipMemcpy(r.cells, cells.data(), sizeof(int) * r.nslow, hipMemcpyHostToDevice));
-    HIPCK(c, hipMalloc(&r.prev, sizeof(float4) * r.nslow));
-    HIPCK(c, hipMemset(r.prev, 0, sizeof(float4) * r.nslow));
-    // which populations each cell takes from an NEE neighbour (the face test of
-    // boundary_stream: q crosses the boundary cell's face, e_q . n == 1), resolved once here
-    // so that the kernel issues every load of such a cell in one round trip
-    std::vector<uint2> nm(cells.size());
-    int64_t off[kQ];
-    for (int q = 0; q < kQ; ++q) {
-      const int s0 = c->L.swap ? kEy[q] : kEx[q], s1 = c->L.swap ? kEx[q] : kEy[q];
-      off[q] = s0 + (int64_t)s1 * c->L.pitch + (int64_t)kEz[q] * c->L.plane;
-    }
-    for (size_t i = 0; i < cells.size(); ++i) {
-      uint32_t nee = 0, press = 0;
-      for (int q = 1; q < kQ; ++q) {
-        const int64_t nb = cells[i] - off[q];
-        if (nb < 0 || nb >= (int64_t)t.size()) continue;
-        const uint8_t tn = t[nb];
-        if ((tn & kClassMask) != kNee) continue;
-        const int fb = (kEx[q] == 1 ? 1 : 0) | (kEx[q] == -1 ? 2 : 0) | (kEy[q] == 1 ? 4 : 0) |
-                       (kEy[q] == -1 ? 8 : 0) | (kEz[q] == 1 ? 16 : 0) | (kEz[q] == -1 ? 32 : 0);
-        if (!((fb >> nee_face(tn)) & 1)) continue;
-        nee |= 1u << q;
-        if (tn & kKindPressure) press |= 1u << q;
-      }
-      nm[i] = make_uint2(nee, press);
-    }
-    // group cells with the same directions (inlet / outlet / lid faces, edges) so that the
-    // lanes of a wave take the same branches; cell order within a group
-    std::vector<size_t> perm(cells.size());
-    for (size_t i = 0; i < perm.size(); ++i) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](size_t x, size_t y) {
-      return nm[x].x != nm[y].x ? nm[x].x < nm[y].x : nm[x].y < nm[y].y;
-    });
-    std::vector<int> sc(cells.size());
-    std::vector<uint2> snm(cells.size());
-    for (size_t i = 0; i < perm.size(); ++i) {
-      sc[i] = cells[perm[i]];
-      snm[i] = nm[perm[i]];
-    }
-    HIPCK(c, hipMemcpy(r.cells, sc.data(), sizeof(int) * r.nslow, hipMemcpyHostToDevice));
-    int64_t adj = 0;  // list neighbours that are storage neighbours (their lanes share lines)
-    for (size_t i = 1; i < sc.size(); ++i) adj += sc[i] == sc[i - 1] + 1;
-    if (sc.size() > 1) contig = (double)adj / (double)(sc.size() - 1);
-    nm.swap(snm);
-    HIPCK(c, hipMalloc(&r.nee_mask, sizeof(uint2) * r.nslow));
-    HIPCK(c, hipMemcpy(r.nee_mask, nm.data(), sizeof(uint2) * r.nslow, hipMemcpyHostToDevice));
-    // the boundary cells' data is written by classification and never changes afterwards
-    HIPCK(c, hipMalloc(&r.nee_bc, sizeof(float4) * kNeeSlots * r.nslow));
-    HIPCK(c, launch_nee_gather(r.cells, r.nee_mask, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.nslow, c->L.pitch,
-                               c->L.plane, c->L.swap, c->s_comp));
-    HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   {
     const int cpl = g_tune[LBM_TUNE_CELLS_PER_LANE];  // A/B switch: 1 or 4 (0: by size)
     r.quarter = cpl ? (cpl == 1) : (r.nchunks <= kQuarterMaxChunks);
   }
   // Lane masks for the 4-cell path: bit l of a chunk's mask is set when lane l (cells 4l ..
-  // 4l+3) holds a cell the chunk wave updates (fluid, in range, not NEE-adjacent) or neighbours
+  // 4l+3) holds a cell the chunk wave updates (fluid, in range) or neighbours
   // such a lane (the DPP x-shift reads the next lanes' slices).  Lanes outside it load nothing:
   // on a vessel tree most chunks are partly empty (the upsampled bifurcation keeps 51% of its
   // active chunks' cells).  Only for sparse chunk lists, whose waves load their chunk id
@@ -460,7 +383,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         for (int k = 0; k < 4; ++k) {
           const int64_t cell = base + 4 * l + k;
           const uint8_t v = t[cell];
-          if (in(cell) && (v & kClassMask) == kFluid && !(v & kNeedsMac)) m |= 1ull << l;
+          if (in(cell) && (v & kClassMask) == kFluid) m |= 1ull << l;
         }
       busy += __builtin_popcountll(m);
       m |= (m << 1) | (m >> 1);
@@ -490,19 +413,13 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       r.stride = true;
     }
   }
-  r.nee_waves = nee_waves_for(r.nslow, contig);
-  r.nee_blocks = nee_grid(r.nslow, r.nee_waves);
-  r.npart = r.main_blocks + r.nee_blocks;
+  r.npart = r.main_blocks;
   return LBM_OK;
 }
 
 void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.lane_masks) (void)hipFree(r.lane_masks);
-  if (r.cells) (void)hipFree(r.cells);
-  if (r.prev) (void)hipFree(r.prev);
-  if (r.nee_mask) (void)hipFree(r.nee_mask);
-  if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
 }
 
@@ -523,9 +440,6 @@ int reset_state(lbm_ctx* c) {
   cs.stag_max = host.stag_max;
   cs.tol = host.tol;
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
-  for (Range* r : {&c->whole, &c->edge, &c->mid}) {
-    if (r->prev) HIPCK(c, hipMemset(r->prev, 0, sizeof(float4) * r->nslow));
-  }
   if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
     HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
     HIPCK(c, hipStreamSynchronize(c->s_comp));
@@ -713,13 +627,15 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   {
     // population buffers (buffer_placement(); LBM_TUNE_BUFFER_ALLOC 1: first two allocations)
     const size_t bytes = sizeof(float) * L.buf_floats();
-    const size_t others = (size_t)L.ncell * (1 + 4 + 16 + 4) + ((size_t)1 << 30);  // type, links, macros, lists
+    const size_t others = (size_t)L.ncell * (1 + 4 + 4 + 16 + 1) + ((size_t)1 << 30);  // type, links, macros, codes
     CK(buffer_placement(c, bytes, others));
     for (int b = 0; b < 2; ++b) c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
   }
   CK(hipMalloc(&c->type, L.ncell));
-  CK(hipMalloc(&c->links, sizeof(uint32_t) * L.ncell));
-  CK(hipMemsetAsync(c->links, 0, sizeof(uint32_t) * L.ncell, c->s_comp));
+  for (uint32_t** p : {&c->links, &c->nlinks}) {
+    CK(hipMalloc(p, sizeof(uint32_t) * L.ncell));
+    CK(hipMemsetAsync(*p, 0, sizeof(uint32_t) * L.ncell, c->s_comp));
+  }
   for (float** p : {&c->rho, &c->ux, &c->uy, &c->uz}) {
     CK(hipMalloc(p, sizeof(float) * L.ncell));
     CK(hipMemsetAsync(*p, 0, sizeof(float) * L.ncell, c->s_comp));
@@ -814,7 +730,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       }
     }
   }
-  g.codes = dcodes; g.type = c->type; g.links = c->links;
+  g.codes = dcodes; g.type = c->type; g.links = c->links; g.nlinks = c->nlinks;
   g.rho = c->rho; g.ux = c->ux; g.uy = c->uy; g.uz = c->uz;
   g.inlet_uy = din; g.outlet_uy = dout;
   g.case_kind = d.case_kind; g.lid_u = d.lid_u;
@@ -837,7 +753,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
           const uint8_t v = t[cell_of(L, x, y, z)];
           if ((v & kClassMask) != kFluid) continue;
           ++nf;
-          if (v & kNeedsMac) ++c->n_slow;
+          if (v & kNeeAdj) ++c->n_slow;
           if (v & kWallAdj) ++c->n_wall_adj;
           // a fluid cell on the outer x/y layer would pull across rows
           if (x == 0 || x == d.nx - 1 || y == 0 || y == d.ny - 1) {
@@ -879,6 +795,7 @@ void lbm_destroy(lbm_ctx* c) {
   for (Range* r : {&c->whole, &c->edge, &c->mid}) free_range(*r);
   if (c->type) (void)hipFree(c->type);
   if (c->links) (void)hipFree(c->links);
+  if (c->nlinks) (void)hipFree(c->nlinks);
   if (c->codes) (void)hipFree(c->codes);
   if (c->bc_in) (void)hipFree(c->bc_in);
   if (c->bc_out) (void)hipFree(c->bc_out);
@@ -1064,15 +981,14 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
 }
 
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
-  int h = c->steps_done;
   if (c->fuse_red && !c->conv_enabled) {
     // one launch per step: step s's k_step also finishes step s-1's residual; the last
     // step's own reduction follows the loop
     const double* prev = nullptr;
-    for (int s = 0; s < nsteps; ++s, ++h) {
+    for (int s = 0; s < nsteps; ++s) {
       double* part = c->red_part + (size_t)(s & 1) * c->red_n;
       const FusedRed fr{part, prev, (want_hist && s > 0) ? c->hist + s - 1 : nullptr};
-      RCK(run_range(c, c->whole, h, c->cur, c->s_comp, &fr));
+      RCK(run_range(c, c->whole, c->cur, c->s_comp, &fr));
       c->cur ^= 1;
       prev = part;
     }
@@ -1080,8 +996,8 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
                            c->s_comp));
     return LBM_OK;
   }
-  for (int s = 0; s < nsteps; ++s, ++h) {
-    RCK(run_range(c, c->whole, h, c->cur, c->s_comp));
+  for (int s = 0; s < nsteps; ++s) {
+    RCK(run_range(c, c->whole, c->cur, c->s_comp));
     c->cur ^= 1;
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
                            1, c->s_comp));
@@ -1100,11 +1016,11 @@ int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
     HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
     // edge planes first, so their halo travels while the interior runs
-    RCK(run_range(c, c->edge, h, c->cur, c->s_comp, nullptr, kKindEdge));
+    RCK(run_range(c, c->edge, c->cur, c->s_comp, nullptr, kKindEdge));
     hipEvent_t halo_end = nullptr;
     RCK(rccl_exchange(c, c->cur ^ 1, false, &halo_end));
     c->last_mid_end = nullptr;
-    RCK(run_range(c, c->mid, h, c->cur, c->s_comp, nullptr, kKindMid));
+    RCK(run_range(c, c->mid, c->cur, c->s_comp, nullptr, kKindMid));
     c->cur ^= 1;
     if (c->prof && halo_end && c->last_mid_end)  // how long the halo outlasts the interior
       c->recs.push_back({c->last_mid_end, halo_end, {kKindExposed, -1, -1}});
@@ -1168,8 +1084,8 @@ int wait_streams(lbm_ctx* c) {
   }
 }
 
-// lazy macros: the (rho, u) the last step computed, from its source buffer (k_moments) and
-// the NEE-adjacent cells' kept values (k_prev_scatter); steps_done is device-confirmed here
+// lazy macros: the (rho, u) the last step computed, from its source buffer (k_moments);
+// steps_done is device-confirmed here
 int refresh_macros(lbm_ctx* c) {
   HIPCK(c, hipSetDevice(c->d.device));
   RCK(wait_streams(c));
@@ -1183,10 +1099,6 @@ int refresh_macros(lbm_ctx* c) {
   const float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
   HIPCK(c, launch_moments(src, c->type, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
                           L.swap, c->s_comp));
-  std::vector<Range*> rs;
-  if (c->last_slab) rs = {&c->edge, &c->mid};
-  else rs = {&c->whole};
-  for (Range* r : rs) HIPCK(c, launch_prev_scatter(r->cells, r->prev, r->nslow, c->rho, c->ux, c->uy, c->uz, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return LBM_OK;
 }
@@ -1216,7 +1128,6 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
   }
   RCK(c->comm ? step_rccl(c, nsteps, want_hist) : step_single(c, nsteps, want_hist));
   c->macros_stale = true;
-  c->last_slab = c->comm != nullptr;
   const bool sync = want_hist || steps_done || c->conv_enabled;
   if (sync) {
     RCK(wait_streams(c));
@@ -1331,25 +1242,19 @@ int lbm_get_f(lbm_ctx* c, float* f) {
 
 namespace {
 
+// version 2: the complete state is the two population buffers (NEE values included, stored
+// producer-side into the boundary cells' slots) plus the run state below
 struct CkptHeader {
   char magic[8];  // "LBMCKPT1"
   int32_t version, nx, ny, nz, z_offset, nz_global, case_kind, swap, pitch, xshift, steps_done, cur;
-  int32_t last_slab;    // the last steps ran the slab ranges: their NEE lists hold the live (rho, u)
   int32_t halo_primed;  // the ghost planes hold the exchange state (all 19 populations only at step 0)
   uint32_t tau_bits;
-  int32_t nslow[3];  // whole, edge, mid NEE-adjacent lists
   int64_t ncell, buf_floats;
   ConvState conv;
 };
+constexpr int32_t kCkptVersion = 2;
 
 constexpr size_t kCkptSlice = (size_t)64 << 20;  // bytes staged through the host per copy
-
-int ckpt_range_lists(lbm_ctx* c, Range* rs[3]) {
-  rs[0] = &c->whole;
-  rs[1] = &c->edge;
-  rs[2] = &c->mid;
-  return LBM_OK;
-}
 
 }  // namespace
 
@@ -1358,16 +1263,13 @@ int lbm_checkpoint_save(lbm_ctx* c, const char* path) {
   RCK(lbm_sync(c));
   CkptHeader h{};
   std::memcpy(h.magic, "LBMCKPT1", 8);
-  h.version = 1;
+  h.version = kCkptVersion;
   h.nx = c->L.nx; h.ny = c->L.ny; h.nz = c->L.nz;
   h.z_offset = c->d.z_offset; h.nz_global = c->d.nz_global; h.case_kind = c->d.case_kind;
   h.swap = c->L.swap; h.pitch = c->L.pitch; h.xshift = c->L.xshift;
-  h.steps_done = c->steps_done; h.cur = c->cur; h.last_slab = c->last_slab ? 1 : 0;
+  h.steps_done = c->steps_done; h.cur = c->cur;
   h.halo_primed = c->halo_primed ? 1 : 0;
   std::memcpy(&h.tau_bits, &c->tau, 4);
-  Range* rs[3];
-  ckpt_range_lists(c, rs);
-  for (int i = 0; i < 3; ++i) h.nslow[i] = rs[i]->nslow;
   h.ncell = c->L.ncell;
   h.buf_floats = c->L.nchunk * kQ * kChunk;
   HIPCK(c, hipMemcpy(&h.conv, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
@@ -1390,8 +1292,6 @@ int lbm_checkpoint_save(lbm_ctx* c, const char* path) {
   // the current state and the buffer the last step read (the lazy macro read-out needs it)
   for (int b : {c->cur, c->cur ^ 1})
     if (rc == LBM_OK) rc = dump(c->buf[b], sizeof(float) * (size_t)h.buf_floats);
-  for (int i = 0; i < 3 && rc == LBM_OK; ++i)
-    if (rs[i]->nslow) rc = dump(rs[i]->prev, sizeof(float4) * (size_t)rs[i]->nslow);
   if (std::fclose(f) != 0) ok = false;
   if (rc != LBM_OK) return rc;
   if (!ok) {
@@ -1410,20 +1310,16 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
     return LBM_ERR_ARG;
   }
   CkptHeader h{};
-  Range* rs[3];
-  ckpt_range_lists(c, rs);
   uint32_t tau_bits;
   std::memcpy(&tau_bits, &c->tau, 4);
-  bool match = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, "LBMCKPT1", 8) == 0 && h.version == 1 &&
+  bool match = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, "LBMCKPT1", 8) == 0 && h.version == kCkptVersion &&
                h.nx == c->L.nx && h.ny == c->L.ny && h.nz == c->L.nz && h.z_offset == c->d.z_offset &&
                h.nz_global == c->d.nz_global && h.case_kind == c->d.case_kind && h.swap == c->L.swap &&
                h.pitch == c->L.pitch && h.xshift == c->L.xshift && h.tau_bits == tau_bits &&
                h.ncell == c->L.ncell && h.buf_floats == c->L.nchunk * kQ * kChunk;
-  for (int i = 0; i < 3 && match; ++i) match = h.nslow[i] == rs[i]->nslow;
   // run state of a well-formed file: one of the two buffers current, flags 0/1, the device
   // step counter equal to the host's
-  const bool sane = (h.cur == 0 || h.cur == 1) && h.steps_done >= 0 && (h.last_slab == 0 || h.last_slab == 1) &&
-                    (h.halo_primed == 0 || h.halo_primed == 1) && h.conv.k == h.steps_done &&
+  const bool sane = (h.cur == 0 || h.cur == 1) && h.steps_done >= 0 && (h.halo_primed == 0 || h.halo_primed == 1) && h.conv.k == h.steps_done &&
                     h.conv.tol_count >= 0 && h.conv.stopped >= 0 && h.conv.stopped <= 2;
   if (match && !sane) {
     std::fclose(f);
@@ -1449,8 +1345,6 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
   int rc = LBM_OK;
   for (int b : {h.cur, h.cur ^ 1})
     if (rc == LBM_OK) rc = fill(c->buf[b], sizeof(float) * (size_t)h.buf_floats);
-  for (int i = 0; i < 3 && rc == LBM_OK; ++i)
-    if (rs[i]->nslow) rc = fill(rs[i]->prev, sizeof(float4) * (size_t)rs[i]->nslow);
   std::fclose(f);
   if (rc != LBM_OK) return rc;
   if (!ok) {
@@ -1473,7 +1367,6 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
   c->cur = h.cur;
   c->steps_done = h.steps_done;
   c->macros_stale = h.steps_done > 0;
-  c->last_slab = h.last_slab != 0;
   // the saved ghost planes are the exchange's own state: after the first step only the 5
   // crossing populations are exchanged, and a ghost wall's other slots hold this slab's
   // bounce-back values, which a fresh 19-population exchange would overwrite
@@ -1745,12 +1638,11 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     RCK(loopback_exchange(cs, n, c0->cur, true, st));
     for (int i = 0; i < n; ++i) cs[i]->halo_primed = true;
   }
-  int h = c0->steps_done;
-  for (int s = 0; s < nsteps; ++s, ++h) {
+  for (int s = 0; s < nsteps; ++s) {
     for (int i = 0; i < n; ++i) {
       lbm_ctx* c = cs[i];
-      RCK(run_range(c, c->edge, h, c0->cur, st));
-      RCK(run_range(c, c->mid, h, c0->cur, st));
+      RCK(run_range(c, c->edge, c0->cur, st));
+      RCK(run_range(c, c->mid, c0->cur, st));
       HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, st));
     }
     RCK(loopback_exchange(cs, n, c0->cur ^ 1, false, st));
@@ -1763,7 +1655,6 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   for (int i = 0; i < n; ++i) {
     cs[i]->steps_done += nsteps;
     cs[i]->macros_stale = true;
-    cs[i]->last_slab = true;
   }
   if (residual_hist && nsteps > 0)
     HIPCK(c0, hipMemcpy(residual_hist, c0->hist, sizeof(float) * nsteps, hipMemcpyDeviceToHost));

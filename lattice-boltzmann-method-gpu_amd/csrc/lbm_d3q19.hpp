@@ -60,10 +60,10 @@ constexpr int face_bits() {
          (Dir<Q>::y == -1 ? 8 : 0) | (Dir<Q>::z == 1 ? 16 : 0) | (Dir<Q>::z == -1 ? 32 : 0);
 }
 
-// Cell-type byte.  bits 0-1 class; fluid: bit 2 has a wall neighbour (bounce-back patched
-// inline by the stream-collide kernel from a per-cell link mask), bit 3 has an NEE neighbour
-// (the cell is re-done by the boundary fix-up kernel, which keeps its previous (rho, u));
-// NEE boundary cell: bits 4-6 face, bit 7 kind (0 velocity, 1 pressure).
+// Cell-type byte.  bits 0-1 class; fluid: bit 2 has a wall neighbour, bit 3 an NEE neighbour
+// supplying one of its populations -- the step kernel stores the bounce-back value / the NEE
+// value into that neighbour's slot producer-side, from per-cell link masks; NEE boundary
+// cell: bits 4-6 face, bit 7 kind (0 velocity, 1 pressure).
 enum : uint8_t {
   kPassive = 0,   // ghost / unused / padding: never updated; pulled raw (constant) if kPulled
   kWall = 1,      // half-way bounce-back
@@ -72,7 +72,7 @@ enum : uint8_t {
   kClassMask = 3,
   kWallAdj = 1u << 2,   // fluid with a wall neighbour
   kPulled = 1u << 2,    // passive cell a fluid cell pulls from (kept constant)
-  kNeedsMac = 1u << 3,  // fluid with an NEE neighbour
+  kNeeAdj = 1u << 3,    // fluid with an NEE neighbour
   kKindPressure = 1u << 7,
 };
 LBM_HD int nee_face(uint8_t t) { return (t >> 4) & 7; }
@@ -156,42 +156,6 @@ LBM_HD float feq_bc(float r, float ux, float uy, float uz) {
 }
 template <> LBM_HD float feq_bc<14>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
   return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz -1.5f* tmp_uy*tmp_uy);
-}
-
-// f^eq_q for a run-time q (1..18), branch-free, bit-identical to feq<q> (bc_form = false)
-// or feq_bc<q> (bc_form = true).  The reference's 18 expression trees share two shapes:
-//   axis q (e along axis a, sign s):  r/18 * (1 + 3A + 3A*A - 1.5 ub*ub - 1.5 uc*uc)
-//   diagonal q (axes a < b, signs):   r/36 * (1 + 3(A+B) + 3A*A + 3B*B + 9A*B - 1.5 uc*uc)
-// with A = s_a u_a, B = s_b u_b and (b, c) / c the remaining axes in x, y, z order.  Signs
-// enter exactly: x - y == x + (-y), -(x + y) == (-x) + (-y), (kx)(-y) == -((kx)y) and
-// addition commutes in IEEE arithmetic, so e.g. "1 - 3(ux+uy)" (q = 10) and
-// "3(uy - ux)" (q = 9) come out bit for bit.  The update form of q = 14 (the one with an
-// fp64 sub-expression) is taken from feq<14> itself.  Checked against every feq<q> /
-// feq_bc<q> on random and special inputs by tests/test_host_ingest.py (tools/feq_rt_check.cpp).
-constexpr uint64_t pack_e(const int* e) {
-  uint64_t p = 0;
-  for (int q = 0; q < 19; ++q) p |= (uint64_t)(e[q] + 1) << (2 * q);
-  return p;
-}
-constexpr uint64_t kPackEx = pack_e(kEx), kPackEy = pack_e(kEy), kPackEz = pack_e(kEz);
-LBM_HD int e_of(uint64_t packed, int q) { return (int)((packed >> (2 * q)) & 3u) - 1; }
-
-LBM_HD float feq_rt(int q, float r, float ux, float uy, float uz, bool bc_form) {
-  if (!bc_form && q == 14) return feq<14>(r, ux, uy, uz);
-  const int ex = e_of(kPackEx, q), ey = e_of(kPackEy, q), ez = e_of(kPackEz, q);
-  if (ex * ex + ey * ey + ez * ez == 1) {
-    const float ua = ex ? ux : ey ? uy : uz;
-    const float A = (ex + ey + ez) < 0 ? -ua : ua;
-    const float ub = ex ? uy : ux;   // a = x: (y, z); a = y: (x, z); a = z: (x, y)
-    const float uc = ez ? uy : uz;
-    return r / 18.0f * (1.0f + 3.0f * A + 3.0f * A * A - 1.5f * ub * ub - 1.5f * uc * uc);
-  }
-  const float ua = ex ? ux : uy;     // first non-zero axis
-  const float ub = ez ? uz : uy;     // second non-zero axis
-  const float uc = !ex ? ux : !ey ? uy : uz;
-  const int sa = ex ? ex : ey, sb = ez ? ez : ey;
-  const float A = sa < 0 ? -ua : ua, B = sb < 0 ? -ub : ub;
-  return r / 36.0f * (1.0f + 3.0f * (A + B) + 3.0f * A * A + 3.0f * B * B + 9.0f * A * B - 1.5f * uc * uc);
 }
 
 // The LDC initialize() form (ldc.cu:542-571): all 19 at once.

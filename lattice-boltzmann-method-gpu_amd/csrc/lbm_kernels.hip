@@ -4,23 +4,23 @@
 // (ldc.cu:57-466, Poiseulle.cu:384-901, bifurcation.cu:429-1023) become one launch of
 // k_step per launch range plus the reduction:
 //
-//  k_step, chunk blocks  one wavefront per 256-cell AoSoA chunk, 4 consecutive cells per
-//                    lane: 19 aligned 16-B pulls issued at once (x neighbours by a DPP lane
-//                    shift, the edge lanes' floats by vector loads that often hit L1), moments,
+//  k_step            one wavefront per 256-cell AoSoA chunk, 4 consecutive cells per lane
+//                    (or, on small lattices, per 64-cell quarter chunk, one cell per lane):
+//                    19 aligned 16-B pulls issued at once (x neighbours by a DPP lane shift,
+//                    the edge lanes' floats by vector loads that often hit L1), moments,
 //                    equilibria and BGK relaxation in registers, 19 16-B stores into the
-//                    chunk.  Half-way bounce-back costs no extra pass and no extra round
-//                    trip: a wall-adjacent cell also stores its outgoing population opp(q)
-//                    into the slot q of the wall it pulls q from next step (producer side;
-//                    the value Poiseulle.cu:601-746 / ldc.cu:184-201 write there), so every
-//                    pull is a plain load.
-//  k_step, NEE blocks    one thread per fluid cell next to an NEE cell (a compact list,
-//                    ~0.2% of the cells at 512^3), which the chunk blocks leave alone:
-//                      NEE cell B at c - e_q with e_q . n_B = 1:
-//                        f_q = feq_q(rho_bc, u_bc) + (src[q][c] - feq_q(rho_c, u_c)) (1 - 1/tau)
-//                        with the cell's own (rho, u) of the previous step (the value
+//                    chunk.  Boundaries cost no extra pass and no extra round trip: the one
+//                    cell that pulls a boundary slot next step stores its value producer side
+//                    --
+//                      wall W = c - e_q:  slot q of W = c's post-collision f_opp(q)
+//                        (the value Poiseulle.cu:601-746 / ldc.cu:184-201 write there);
+//                      NEE cell B = c - e_q with e_q . n_B = 1:  slot q of B =
+//                        feq_q(rho_bc, u_bc) + (f'_q(c) - feq_q(rho_c, u_c)) (1 - 1/tau)
+//                        with c's post-collision f'_q and (rho, u) of this step (the value
 //                        boundary_stream writes into B, ldc.cu:391-456, Poiseulle.cu:748-891,
 //                        bifurcation.cu:877-1021; their hand-simplified "tmp" terms are
-//                        bit-identical to feq_q(rho_bc, u_bc)).
+//                        bit-identical to feq_q(rho_bc, u_bc)) --
+//                    so every pull is a plain load and every fluid cell an ordinary lane.
 //  residual          the |u| partials of a step (one per block) are summed in a fixed order
 //                    by the first block of the NEXT step's launch, which then runs the
 //                    residual / convergence logic of ldc.cu:660-684 on the device, so a step
@@ -231,8 +231,135 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
   return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f;  // false for NaN
 }
 
-// One wave's chunk: pull, collide, store; returns the lane's |u| sum.  NEE-adjacent cells
-// are left to the NEE blocks of the same launch (nee_cell).
+// ---- NEE boundaries, producer side -------------------------------------------------------
+// boundary_stream (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021) writes,
+// after the collision, into each NEE cell B and direction q crossing B's face (nb = B + e_q):
+//   dst[q][B] = feq_q(rho_bc, u_bc) + (dst[q][nb] - feq_q(rho_nb, u_nb)) (1 - 1/tau)
+// Only nb pulls slot q of B (from nb - e_q = B), and nb holds every operand right after its
+// own collision: its post-collision f_q and its (rho, u) of the step.  So nb -- the fluid
+// cell c of the kernels, B = c - e_q -- stores the value itself, as it stores its bounce-back
+// slots.  B's boundary data (written at B by k_classify, static): rho_bc or NaN (rho of c),
+// u_bc or NaN (a pressure boundary: u of c).
+
+constexpr uint64_t pack_e(const int* e) {
+  uint64_t p = 0;
+  for (int q = 0; q < kQ; ++q) p |= (uint64_t)(e[q] + 1) << (2 * q);
+  return p;
+}
+constexpr uint64_t kPackEx = pack_e(kEx), kPackEy = pack_e(kEy), kPackEz = pack_e(kEz);
+__device__ __forceinline__ int e_of(uint64_t packed, int q) { return (int)((packed >> (2 * q)) & 3u) - 1; }
+
+template <bool SW>
+__device__ __forceinline__ int64_t cell_off_rt(int q, int pitch, int64_t plane) {
+  const int ex = e_of(kPackEx, q), ey = e_of(kPackEy, q), ez = e_of(kPackEz, q);
+  return (SW ? ey : ex) + (int64_t)(SW ? ex : ey) * pitch + (int64_t)ez * plane;
+}
+
+// NEE directions of a cell whose boundary data is loaded ahead (one flat face: 5); a cell
+// with more (edges and corners of several faces) loads the rest where they are used
+constexpr int kNeeSlots = 5;
+
+__device__ __forceinline__ float4 bc_at(const MainArgs& a, int64_t b) {
+  return make_float4(a.rho[b], a.ux[b], a.uy[b], a.uz[b]);
+}
+
+// The boundary data of a cell's first kNeeSlots NEE directions (ascending q), loaded ahead
+// -- all issued together, one round trip.  Named members, not an array: a select over an
+// array's elements is folded into a dynamic index, which keeps the array in scratch.
+struct BcSlots {
+  float4 s0, s1, s2, s3, s4;
+};
+static_assert(kNeeSlots == 5, "BcSlots holds kNeeSlots records");
+
+template <bool SW>
+__device__ __forceinline__ float4 bc_next(const MainArgs& a, int64_t c, uint32_t& rest) {
+  if (!rest) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const int q = __builtin_ctz(rest);
+  rest &= rest - 1u;
+  return bc_at(a, c - cell_off_rt<SW>(q, a.pitch, a.plane));
+}
+template <bool SW>
+__device__ __forceinline__ BcSlots nee_prefetch(const MainArgs& a, int64_t c, uint32_t nl) {
+  BcSlots b;
+  uint32_t rest = nl;
+  b.s0 = bc_next<SW>(a, c, rest);
+  b.s1 = bc_next<SW>(a, c, rest);
+  b.s2 = bc_next<SW>(a, c, rest);
+  b.s3 = bc_next<SW>(a, c, rest);
+  b.s4 = bc_next<SW>(a, c, rest);
+  return b;
+}
+
+template <int Q>
+__device__ __forceinline__ float nee_value(float fq, float4 b, float r, float ux, float uy, float uz, float omc) {
+  float rb = b.x, bx = b.y, by = b.z, bz = b.w;
+  if (__builtin_isnan(bx)) {  // pressure boundary: u_bc = u of the fluid neighbour
+    bx = ux; by = uy; bz = uz;
+  }
+  if (__builtin_isnan(rb)) rb = r;  // velocity boundary: rho_bc = rho of the fluid neighbour
+  const float e_bc = feq_bc<Q>(rb, bx, by, bz);
+  const float e_nb = feq<Q>(r, ux, uy, uz);
+  return e_bc + (fq - e_nb) * omc;
+}
+
+// the cell's post-collision f_Q, for nee_store_q:
+//  Post1: one cell in registers after its relaxation;
+//  Pre4:  cell j of a 4-cell lane before the relaxation -- f_Q relaxed here by the same
+//         expression as relax_cell (fast: the 3-VALU quotient), so the bits agree
+struct Post1 {
+  const float* f;
+  template <int Q>
+  __device__ __forceinline__ float post(const MainArgs&, float, float, float, float) const {
+    return f[Q];
+  }
+};
+__device__ __forceinline__ float sel4(f4 v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
+struct Pre4 {
+  const f4* v;
+  int j;
+  bool fast;
+  template <int Q>
+  __device__ __forceinline__ float post(const MainArgs& a, float r, float ux, float uy, float uz) const {
+    const float f = sel4(v[Q], j);
+    const float x = f - feq<Q>(r, ux, uy, uz);
+    if (fast) {
+      const float q0 = x * a.tau_rcp;
+      return f - __builtin_fmaf(__builtin_fmaf(-q0, a.tau, x), a.tau_rcp, q0);
+    }
+    return f - x / a.tau;
+  }
+};
+
+template <int Q, bool SW, class Src>
+__device__ __forceinline__ void nee_store_q(const MainArgs& a, int64_t c, uint32_t nl, float4 b0, float4 b1, float4 b2,
+                                            float4 b3, float4 b4, const Src& src, float r, float ux, float uy,
+                                            float uz) {
+  if constexpr (Q > 0) {
+    if (nl & (1u << Q)) {  // divergent only where a wave mixes faces (edges, corners)
+      const int k = __builtin_popcount(nl & ((1u << Q) - 1u));  // Q's slot
+      const int64_t nb = c - cell_off<Q, SW>(a.pitch, a.plane);
+      float4 b;
+      if (k >= kNeeSlots) b = bc_at(a, nb);
+      else b = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : k == 3 ? b3 : b4;
+      const float fq = src.template post<Q>(a, r, ux, uy, uz);
+      a.dst[aidx(nb, Q)] = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc);
+    }
+  }
+}
+
+__device__ __forceinline__ void opaque(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+template <bool SW, class Src, int... Qs>
+__device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint32_t nl, BcSlots bc, const Src& src,
+                                              float r, float ux, float uy, float uz, std::integer_sequence<int, Qs...>) {
+  // plain registers from here on: otherwise the slot selections below fold into one load at
+  // a variable offset, and the records go through scratch
+  float4 b0 = bc.s0, b1 = bc.s1, b2 = bc.s2, b3 = bc.s3, b4 = bc.s4;
+  opaque(b0); opaque(b1); opaque(b2); opaque(b3); opaque(b4);
+  (nee_store_q<Qs, SW>(a, c, nl, b0, b1, b2, b3, b4, src, r, ux, uy, uz), ...);
+}
+
+// One wave's chunk: pull, collide, store; returns the lane's |u| sum.
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
 //        branch) the exact division, counted in exact_waves.  Both paths cost 216-220 VGPRs
 //        against 170 for one -- no occupancy change: either way two waves per SIMD.
@@ -247,15 +374,20 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   pull4_all<SW>(v, a.src, cb, c, lane, a.pitch, a.plane, need, AllQ{});
   const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
   const unsigned t4 = need ? t4r : 0u;
-  // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
-  // so this dependent load hides behind the arithmetic)
-  constexpr unsigned kWall4 = kWallAdj * 0x01010101u;
-  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+  // wall- and NEE-link masks of the lane's boundary-adjacent cells (a dependent load, rare)
+  constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
+  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0;
   if (t4 & kWall4) {
     if (t4 & (kWallAdj << 0)) m0 = a.links[c + 0];
     if (t4 & (kWallAdj << 8)) m1 = a.links[c + 1];
     if (t4 & (kWallAdj << 16)) m2 = a.links[c + 2];
     if (t4 & (kWallAdj << 24)) m3 = a.links[c + 3];
+  }
+  if (t4 & kNee4) {
+    if (t4 & (kNeeAdj << 0)) n0 = a.nlinks[c + 0];
+    if (t4 & (kNeeAdj << 8)) n1 = a.nlinks[c + 1];
+    if (t4 & (kNeeAdj << 16)) n2 = a.nlinks[c + 2];
+    if (t4 & (kNeeAdj << 24)) n3 = a.nlinks[c + 3];
   }
   float r0, r1, r2, r3, x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
   moments<0>(v, r0, x0, y0, z0);
@@ -281,8 +413,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   for (int j = 0; j < 4; ++j) {
     const unsigned t = (t4 >> (8 * j)) & 0xffu;
     const int64_t cj = c + j;
-    const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
-                    !(t & kNeedsMac);
+    const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid;
     if (in) {
       store |= 1u << j;
       acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
@@ -296,8 +427,26 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
   const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
-  const bool keep_others = special != 0u || !lane_in || (t4 & (kNeedsMac * 0x01010101u));
+  const bool keep_others = special != 0u || !lane_in;
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
+  // NEE values of the lane's NEE-adjacent cells (rare, divergent), before the relaxation so
+  // that the moments need not outlive it: cell j's f_q is relaxed once more here by the same
+  // expression.  One cell at a time keeps one copy of the 18-direction code and few registers.
+  if (t4 & kNee4) {
+    unsigned nee = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (((store >> j) & 1u) && ((t4 >> (8 * j)) & kNeeAdj)) nee |= 1u << j;
+    const f4 RH{r0, r1, r2, r3};
+#pragma unroll 1
+    for (; nee; nee &= nee - 1u) {
+      const int j = __builtin_ctz(nee);
+      const uint32_t nl = j == 0 ? n0 : j == 1 ? n1 : j == 2 ? n2 : n3;
+      const BcSlots bc = nee_prefetch<SW>(a, c + j, nl);
+      nee_store_all<SW>(a, c + j, nl, bc, Pre4{v, j, FAST && fast_wave}, sel4(RH, j), sel4(UX, j), sel4(UY, j),
+                        sel4(UZ, j), AllQ{});
+    }
+  }
   if (FAST && fast_wave) {
     relax_cell<0, true>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
     relax_cell<1, true>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
@@ -330,147 +479,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   return acc;
 }
 
-// ---- NEE-adjacent cells ----------------------------------------------------------------
-
-struct Macro {
-  float rho, ux, uy, uz;
-};
-
-// NEE-supplied pulls (boundary cell B = c - e_q with e_q . n_B == 1), in two phases so
-// that all of a cell's loads are in flight together: which q come from an NEE neighbour is
-// static (nee_mask, built with the work lists), so no load waits on another.
-//   issue: the 19 pulls, and for the first kNeeSlots NEE directions the cell's own src
-//          slot and B's boundary data (u_bc, and rho_bc or NaN; a pressure cell's rho_bc);
-//   apply: f_q = feq_q(rho_bc, u_bc) + (own - feq_q(rho_c, u_c)) (1 - 1/tau), with the
-//          cell's own (rho, u) of the previous step.
-// A cell beside one flat face has 5 NEE directions; cells with more (edges, corners of
-// several boundary faces) load the rest where they are used.
-
-template <bool SW>
-__device__ __forceinline__ int64_t cell_off_rt(int q, int pitch, int64_t plane) {
-  const int ex = e_of(kPackEx, q), ey = e_of(kPackEy, q), ez = e_of(kPackEz, q);
-  return (SW ? ey : ex) + (int64_t)(SW ? ex : ey) * pitch + (int64_t)ez * plane;
-}
-
-struct NeeSlot {
-  float own, r, x, y, z;
-};
-
-template <bool SW>
-__device__ __forceinline__ NeeSlot nee_load(const MainArgs& a, int64_t c, int64_t nb, int q) {
-  return NeeSlot{a.src[aidx(c, q)], a.rho[nb], a.ux[nb], a.uy[nb], a.uz[nb]};
-}
-__device__ __forceinline__ NeeSlot nee_slot(float own, const float4 b) { return NeeSlot{own, b.x, b.y, b.z, b.w}; }
-
-// the NEE value of direction Q from its slot
-template <int Q>
-__device__ __forceinline__ float nee_value(const NeeSlot& d, const Macro& mp, bool pressure, float omc) {
-  float rb = d.r, bx, by, bz;
-  if (pressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
-    bx = mp.ux; by = mp.uy; bz = mp.uz;
-  } else {         // u_bc stored at B; rho_bc too, or NaN: that of the fluid cell
-    if (__builtin_isnan(rb)) rb = mp.rho;
-    bx = d.x; by = d.y; bz = d.z;
-  }
-  const float e_bc = feq_bc<Q>(rb, bx, by, bz);
-  const float e_nb = feq<Q>(mp.rho, mp.ux, mp.uy, mp.uz);
-  return e_bc + (d.own - e_nb) * omc;
-}
-
-// run-time q (the slot's direction): the branch-free feq_rt, so lanes with different
-// directions stay together
-__device__ __forceinline__ float nee_value_rt(int q, const NeeSlot& d, const Macro& mp, bool pressure, float omc) {
-  float rb = d.r, bx, by, bz;
-  if (pressure) {  // rho_bc stored at B; u_bc = u of the fluid neighbour
-    bx = mp.ux; by = mp.uy; bz = mp.uz;
-  } else {         // u_bc stored at B; rho_bc too, or NaN: that of the fluid cell
-    if (__builtin_isnan(rb)) rb = mp.rho;
-    bx = d.x; by = d.y; bz = d.z;
-  }
-  const float e_bc = feq_rt(q, rb, bx, by, bz, true);
-  const float e_nb = feq_rt(q, mp.rho, mp.ux, mp.uy, mp.uz, false);
-  return e_bc + (d.own - e_nb) * omc;
-}
-
-// f[Q] from the k-th NEE value (k = rank of Q among the cell's NEE directions)
-template <int Q, bool SW>
-__device__ __forceinline__ void nee_put(float* f, const float* nv, const MainArgs& a, int64_t c, const Macro& mp,
-                                        uint32_t nee, uint32_t press) {
-  if constexpr (Q > 0) {
-    if (nee & (1u << Q)) {
-      const int k = __builtin_popcount(nee & ((1u << Q) - 1u));
-      float v = nv[0];
-#pragma unroll
-      for (int j = 1; j < kNeeSlots; ++j)
-        if (k == j) v = nv[j];
-      if (k >= kNeeSlots)  // beyond the slots (edges/corners of several faces): load here
-        v = nee_value<Q>(nee_load<SW>(a, c, c - cell_off<Q, SW>(a.pitch, a.plane), Q), mp, (press >> Q) & 1u,
-                         a.omc);
-      f[Q] = v;
-    }
-  }
-}
-
-template <bool SW, int... Qs>
-__device__ __forceinline__ void nee_pull_all(float* f, const MainArgs& a, int64_t c, const Macro& mp, uint2 m,
-                                             const float4* bc, std::integer_sequence<int, Qs...>) {
-  const uint32_t nee = a.nee_active ? m.x : 0u;
-  NeeSlot sl[kNeeSlots];
-  int qs[kNeeSlots];
-  uint32_t rest = nee;
-#pragma unroll
-  for (int j = 0; j < kNeeSlots; ++j) {
-    qs[j] = 0;
-    if (rest) {
-      const int q = __builtin_ctz(rest);
-      rest &= rest - 1u;
-      qs[j] = q;
-      sl[j] = nee_slot(a.src[aidx(c, q)], bc[j]);
-    }
-  }
-  ((f[Qs] = a.src[aidx(c - cell_off<Qs, SW>(a.pitch, a.plane), Qs)]), ...);
-  if (!nee) return;
-  float nv[kNeeSlots];
-#pragma unroll
-  for (int j = 0; j < kNeeSlots; ++j)
-    nv[j] = qs[j] ? nee_value_rt(qs[j], sl[j], mp, (m.y >> qs[j]) & 1u, a.omc) : 0.f;
-  (nee_put<Qs, SW>(f, nv, a, c, mp, nee, m.y), ...);
-}
-
-// Cells beside one flat boundary face (nearly all NEE-adjacent cells; the list is grouped by
-// direction mask, so whole waves share one) take all five directions of that face: the
-// j-th direction is a compile-time q, the NEE value the compile-time feq_bc<q> / feq<q> trees
-// (the same expressions feq_rt evaluates at run time), and no slot selection is needed.
-constexpr bool crosses_face(int q, int f) {
-  const int e = f < 2 ? kEx[q] : f < 4 ? kEy[q] : kEz[q];
-  return e == ((f & 1) ? -1 : 1);
-}
-constexpr int face_q(int f, int j) {  // the j-th (ascending) direction crossing face f
-  int k = 0;
-  for (int q = 1; q < kQ; ++q)
-    if (crosses_face(q, f)) {
-      if (k == j) return q;
-      ++k;
-    }
-  return 0;
-}
-constexpr uint32_t face_set(int f) {
-  uint32_t m = 0;
-  for (int q = 1; q < kQ; ++q)
-    if (crosses_face(q, f)) m |= 1u << q;
-  return m;
-}
-
-template <int F, bool SW, int... Js, int... Qs>
-__device__ __forceinline__ void nee_pull_face(float* f, const MainArgs& a, int64_t c, const Macro& mp, uint32_t press,
-                                              const float4* bc, std::integer_sequence<int, Js...>,
-                                              std::integer_sequence<int, Qs...>) {
-  float own[kNeeSlots];
-  ((own[Js] = a.src[aidx(c, face_q(F, Js))]), ...);
-  ((f[Qs] = a.src[aidx(c - cell_off<Qs, SW>(a.pitch, a.plane), Qs)]), ...);
-  ((f[face_q(F, Js)] = nee_value<face_q(F, Js)>(nee_slot(own[Js], bc[Js]), mp, (press >> face_q(F, Js)) & 1u, a.omc)),
-   ...);
-}
+// ---- one cell per lane ---------------------------------------------------------------
 
 template <int... Qs>
 __device__ __forceinline__ void fix_relax_all(float* f, float tau, float r, float ux, float uy, float uz,
@@ -512,46 +521,6 @@ __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict_
   if (m) (bb_store_one<Qs, SW>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
 }
 
-// One NEE-adjacent fluid cell (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021
-// applied on the consumer side): its pulls with the NEE value substituted for every
-// population an NEE neighbour supplies, collide (exact division), store incl. its own
-// bounce-back slots, keep its (rho, u) for the next step's NEE values.
-template <bool SW>
-__device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
-  const int64_t c = a.cells[i];
-  const float4 pv = a.prev[i];
-  const Macro mp{pv.x, pv.y, pv.z, pv.w};
-  const uint2 mk = a.nee_mask[i];
-  float4 bc[kNeeSlots];  // static boundary data: no wait on the cell id
-#pragma unroll
-  for (int j = 0; j < kNeeSlots; ++j) bc[j] = a.nee_bc[(int64_t)i * kNeeSlots + j];
-  const uint32_t links = a.links[c];
-  float f[kQ];
-  // a wave whose cells all sit beside one flat y face -- the reference's lid (ldc.cu:391-456),
-  // inlet and outlet (Poiseulle.cu:748-891, bifurcation.cu:877-1021) -- takes that face's
-  // specialised path.  Only the two y faces: the step kernels are latency-bound at the sizes
-  // where NEE cells matter, and six specialisations grew k_step1 by half and gave the
-  // bifurcation's gain back (C4 10.8 vs 11.7 us per step, LDC 64^3 11.9 either way); one
-  // shared moments / relaxation tail for fluid and NEE cells was slower too (12.3 / 10.9 us).
-  const uint32_t nee = a.nee_active ? mk.x : 0u;
-  const uint32_t nee0 = __builtin_amdgcn_readfirstlane(nee);
-  const bool uniform = __all(nee == nee0);
-  using Five = std::make_integer_sequence<int, kNeeSlots>;
-  if (uniform && nee0 == face_set(kFacePY)) nee_pull_face<kFacePY, SW>(f, a, c, mp, mk.y, bc, Five{}, AllQ{});
-  else if (uniform && nee0 == face_set(kFaceNY)) nee_pull_face<kFaceNY, SW>(f, a, c, mp, mk.y, bc, Five{}, AllQ{});
-  else nee_pull_all<SW>(f, a, c, mp, mk, bc, AllQ{});
-  float rho = 0.f;
-#pragma unroll
-  for (int q = 0; q < kQ; ++q) rho = rho + f[q];
-  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
-  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
-  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  relax1(f, a, rho, ux, uy, uz);
-  fix_store_all<SW>(f, a.dst, c, links, a.pitch, a.plane, AllQ{});
-  a.prev[i] = make_float4(rho, ux, uy, uz);  // also the cell's macros (read out lazily)
-  return (double)sqrtf(ux * ux + uy * uy + uz * uz);
-}
-
 // One cell per lane (small lattices: a wave per 64 cells, so 4x the waves of the chunk path
 // and a quarter of its per-wave latency): plain pulls, exact division, bounce-back slots.
 template <bool SW, int... Qs>
@@ -583,11 +552,15 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, i
   const int64_t c = ch * kChunk + l;
   const uint8_t t = a.type[c];
   const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
+  const uint32_t nl = a.nlinks[c];
   float f[kQ];
   pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
-  const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid &&
-                  !(t & kNeedsMac);
+  const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid;
   if (!in) return 0.0;
+  // NEE-adjacent: the boundary data goes out now and arrives under the arithmetic below
+  const bool nee = (t & kNeeAdj) != 0;
+  BcSlots bc{};
+  if (nee) bc = nee_prefetch<SW>(a, c, nl);
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
@@ -595,6 +568,7 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, i
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   relax1(f, a, rho, ux, uy, uz);
+  if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, AllQ{});
   fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
@@ -643,13 +617,13 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       }
       __syncthreads();  // red[] reuse below
     }
-  } else if (bx >= a.nee_blocks) {
+  } else {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own
     // L2), so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of
     // chunks and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
-    const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
+    const int b = bx;  // red_blocks is a multiple of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
@@ -667,12 +641,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
       acc = process_chunk<FAST, SW, MASK>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base
     }
-    slot += a.red_blocks + a.nee_blocks;
-  } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
-    slot = blockIdx.x;
-    const int w = (int)threadIdx.x >> 6;
-    const int i = (bx * a.nee_waves + w) * 64 + ((int)threadIdx.x & 63);
-    if (w < a.nee_waves && i < a.n_nee) acc = nee_cell<SW>(a, i);
+    slot += a.red_blocks;
   }
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[slot] = s;
@@ -803,7 +772,8 @@ __device__ __forceinline__ CellPos cell_pos(int64_t c, int shift, int pitch, int
   return p;
 }
 
-// reference code -> class/face/kind; NEE data into the macro arrays of NEE cells
+// reference code -> class/face/kind; NEE data into the macro arrays of NEE cells (read by the
+// fluid neighbours that store their NEE values, nee_store_q)
 __global__ void k_classify(const GeoArgs g) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < g.ncell;
        c += (int64_t)gridDim.x * blockDim.x) {
@@ -812,7 +782,9 @@ __global__ void k_classify(const GeoArgs g) {
     const int x = p.x, zs = p.zs;
     const int zg = zs - 1 + g.z_offset;  // global z
     uint8_t t = kPassive;
-    const float kRhoOfFluid = __builtin_nanf("");  // rho slot of a velocity NEE cell: use rho_F
+    // NaN in the rho slot of a velocity boundary: rho_bc is the fluid neighbour's; NaN in the u
+    // slots of a pressure boundary: u_bc is the fluid neighbour's (nee_value)
+    const float kRhoOfFluid = __builtin_nanf(""), kUOfFluid = __builtin_nanf("");
     if (p.in && zs < g.planes) {
       const int y = p.y;
       if (g.case_kind == 0) {  // LDC (ldc.cu:469): 0 ghost, 1 wall, 2 lid, 3 fluid
@@ -838,6 +810,7 @@ __global__ void k_classify(const GeoArgs g) {
               v[axis] = b.table[ti];
             }
             g.rho[c] = b.kind == 0 ? kRhoOfFluid : b.rho;
+            if (b.kind == 2) v[0] = v[1] = v[2] = kUOfFluid;
             g.ux[c] = v[0]; g.uy[c] = v[1]; g.uz[c] = v[2];
             break;
           }
@@ -857,7 +830,7 @@ __global__ void k_classify(const GeoArgs g) {
             g.rho[c] = kRhoOfFluid; g.ux[c] = 0.f; g.uy[c] = v; g.uz[c] = 0.f;
           } else {                 // bifurcation: pressure, rho = 1 (bifurcation.cu:890)
             t = make_nee(kFaceNY, true);
-            g.rho[c] = 1.0f; g.ux[c] = 0.f; g.uy[c] = 0.f; g.uz[c] = 0.f;
+            g.rho[c] = 1.0f; g.ux[c] = kUOfFluid; g.uy[c] = kUOfFluid; g.uz[c] = kUOfFluid;
           }
         }
       }
@@ -868,7 +841,7 @@ __global__ void k_classify(const GeoArgs g) {
 
 template <int Q, bool SW>
 __device__ __forceinline__ void scan_nb(const uint8_t* type, int64_t c, const GeoArgs& g, uint8_t& flags,
-                                        uint32_t& walls) {
+                                        uint32_t& walls, uint32_t& nees) {
   const int64_t nb = c - cell_off<Q, SW>(g.pitch, g.plane);
   if (Q == 0 || nb < 0 || nb >= g.ncell) return;
   const uint8_t tn = type[nb];
@@ -877,13 +850,17 @@ __device__ __forceinline__ void scan_nb(const uint8_t* type, int64_t c, const Ge
     flags |= kWallAdj;
     walls |= 1u << Q;
   }
-  if (cls == kNee && ((face_bits<Q>() >> nee_face(tn)) & 1)) flags |= kNeedsMac;
+  // an NEE cell supplies q when q crosses its face (boundary_stream's direction sets)
+  if (cls == kNee && ((face_bits<Q>() >> nee_face(tn)) & 1)) {
+    flags |= kNeeAdj;
+    nees |= 1u << Q;
+  }
 }
 
 template <bool SW, int... Qs>
 __device__ __forceinline__ void scan_all(const uint8_t* type, int64_t c, const GeoArgs& g, uint8_t& flags,
-                                         uint32_t& walls, std::integer_sequence<int, Qs...>) {
-  (scan_nb<Qs, SW>(type, c, g, flags, walls), ...);
+                                         uint32_t& walls, uint32_t& nees, std::integer_sequence<int, Qs...>) {
+  (scan_nb<Qs, SW>(type, c, g, flags, walls, nees), ...);
 }
 
 template <bool SW>
@@ -893,10 +870,11 @@ __global__ void k_flag_fluid(const GeoArgs g) {
     const uint8_t t = g.type[c];
     if ((t & kClassMask) != kFluid) continue;
     uint8_t flags = 0;
-    uint32_t walls = 0;
-    scan_all<SW>(g.type, c, g, flags, walls, AllQ{});
+    uint32_t walls = 0, nees = 0;
+    scan_all<SW>(g.type, c, g, flags, walls, nees, AllQ{});
     g.type[c] = (uint8_t)(t | flags);
     g.links[c] = walls;
+    g.nlinks[c] = nees;
   }
 }
 
@@ -1071,14 +1049,14 @@ __global__ void k_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshif
 // The step kernels store no macros.  lbm_get_macros recomputes the last step's (rho, u) of
 // every fluid cell from that step's source buffer, which the step left intact (A-B
 // pattern): the same 19 pulls and the same fp32 sums as process_chunk / process_cell1, so
-// the bits are those the step used.  NEE-adjacent cells pulled NEE values, not raw slots:
-// their macros are the (rho, u) the step kept in the range's prev list (k_prev_scatter).
+// the bits are those the step used (NEE values included: they sit in the boundary cells'
+// slots of that buffer, stored there by the step before).
 template <bool SW>
 __global__ void k_moments(const float* __restrict__ src, const uint8_t* __restrict__ type, float* rho, float* ux,
                           float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane) {
   for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
     const uint8_t t = type[c];
-    if ((t & kClassMask) != kFluid || (t & kNeedsMac)) continue;
+    if ((t & kClassMask) != kFluid) continue;
     float f[kQ];
     pull1_all<SW>(f, src, c, pitch, plane, AllQ{});
     float r = 0.f;
@@ -1089,15 +1067,6 @@ __global__ void k_moments(const float* __restrict__ src, const uint8_t* __restri
     uy[c] = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / r;
     uz[c] = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / r;
   }
-}
-
-__global__ void k_prev_scatter(const int* __restrict__ cells, const float4* __restrict__ prev, int n, float* rho,
-                               float* ux, float* uy, float* uz) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int64_t c = cells[i];
-  const float4 p = prev[i];
-  rho[c] = p.x; ux[c] = p.y; uy[c] = p.z; uz[c] = p.w;
 }
 
 // ---- field digest ------------------------------------------------------------------------
@@ -1168,14 +1137,11 @@ int main_grid(int nchunks, bool quarter) {
   const int waves = quarter ? 4 * nchunks : nchunks;
   return nchunks ? std::max(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
 }
-// NEE blocks of k_step (first in the grid): a multiple of 8 so the chunk blocks keep their XCD
-int nee_waves_for(int n, double contiguous) { return (n <= 16384 && contiguous < 0.5) ? 1 : kBlock / 64; }
-int nee_grid(int n, int waves) { return (n + 8 * 64 * waves - 1) / (8 * 64 * waves) * 8; }
 
 // Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one);
 // the 4-cell kernel's register count (214 VGPRs, kernel-resource-usage) gives exactly that.
 hipError_t launch_step(const MainArgs& a, hipStream_t s) {
-  const dim3 grid(a.red_blocks + a.main_blocks + a.nee_blocks);
+  const dim3 grid(a.red_blocks + a.main_blocks);
   typedef void (*Kern)(const MainArgs);
   const bool sw = a.swap != 0;
   Kern k;
@@ -1319,50 +1285,12 @@ hipError_t launch_probe_fill(void* dst, int64_t n4, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool SW>
-__global__ void k_nee_gather(const int* __restrict__ cells, const uint2* __restrict__ mask,
-                             const float* __restrict__ rho, const float* __restrict__ ux,
-                             const float* __restrict__ uy, const float* __restrict__ uz, float4* __restrict__ out,
-                             int n, int pitch, int64_t plane) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int64_t c = cells[i];
-  uint32_t rest = mask[i].x;
-  for (int j = 0; j < kNeeSlots; ++j) {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rest) {
-      const int q = __builtin_ctz(rest);
-      rest &= rest - 1u;
-      const int64_t nb = c - cell_off_rt<SW>(q, pitch, plane);
-      v = make_float4(rho[nb], ux[nb], uy[nb], uz[nb]);
-    }
-    out[(int64_t)i * kNeeSlots + j] = v;
-  }
-}
-
-hipError_t launch_nee_gather(const int* cells, const uint2* mask, const float* rho, const float* ux,
-                             const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
-                             int swap, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  const dim3 g((n + 255) / 256);
-  if (swap) hipLaunchKernelGGL(k_nee_gather<true>, g, dim3(256), 0, s, cells, mask, rho, ux, uy, uz, nee_bc, n, pitch, plane);
-  else hipLaunchKernelGGL(k_nee_gather<false>, g, dim3(256), 0, s, cells, mask, rho, ux, uy, uz, nee_bc, n, pitch, plane);
-  return hipGetLastError();
-}
-
 hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
                           int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
   if (hi <= lo) return hipSuccess;
   const dim3 g(grid_for(hi - lo, 256));
   if (swap) hipLaunchKernelGGL(k_moments<true>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
   else hipLaunchKernelGGL(k_moments<false>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
-  return hipGetLastError();
-}
-
-hipError_t launch_prev_scatter(const int* cells, const float4* prev, int n, float* rho, float* ux, float* uy,
-                               float* uz, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prev_scatter, dim3((n + 255) / 256), dim3(256), 0, s, cells, prev, n, rho, ux, uy, uz);
   return hipGetLastError();
 }
 

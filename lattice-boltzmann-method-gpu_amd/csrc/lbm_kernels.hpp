@@ -43,21 +43,22 @@ struct Layout {
   int64_t buf_floats() const { return (nchunk + 2 * guard) * kQ * kChunk; }
 };
 
-// One time step of one launch range, ONE kernel launch (k_step):
-//  * blocks [0, nee_blocks): one thread per NEE-adjacent fluid cell, done with the NEE
-//    values of its boundary neighbours (and its own bounce-back slots);
-//  * blocks [nee_blocks, nee_blocks + main_blocks): fused pull-stream + BGK collide, one
-//    wavefront per active 256-cell chunk, every neighbour a plain pull, wall bounce-back
-//    stored producer-side; stores every fluid cell of the range except the NEE-adjacent
-//    ones -- disjoint cells, so both parts run concurrently.
-// Partials: one fp64 |u| sum per block (reduction blocks, NEE blocks, then chunk blocks).
+// One time step of one launch range, ONE kernel launch (k_step): fused pull-stream + BGK
+// collide, one wavefront per active 256-cell chunk (or 64-cell quarter chunk), every
+// neighbour a plain pull.  Boundary values are stored producer-side into the slots their one
+// consumer pulls next step: wall bounce-back, and the NEE value of an NEE neighbour.
+// Partials: one fp64 |u| sum per block (reduction blocks, then chunk blocks).
 struct MainArgs {
   const float* src;     // base (past the guard chunk)
   float* dst;
   const uint8_t* type;  // per cell
   const uint32_t* links;  // per cell: bit q set when c - e_q is a wall (read for kWallAdj cells)
                           // -> producer-side bounce-back stores
-  float* rho; float* ux; float* uy; float* uz;  // full fields; NEE data sits at NEE cells
+  const uint32_t* nlinks;  // per cell: bit q set when c - e_q is an NEE cell supplying q (face
+                           // match; read for kNeeAdj cells) -> producer-side NEE stores
+  const float* rho; const float* ux; const float* uy; const float* uz;  // NEE data at NEE cells:
+                        // rho_bc or NaN (rho of the fluid neighbour), u_bc or NaN (pressure
+                        // boundary: u of the fluid neighbour)
   double* partial;      // one per block
   const int* chunks;    // active chunk ids
   int chunk0;           // >= 0: they are chunk0, chunk0 + 1, ... (box lattices) -- no list load,
@@ -83,18 +84,6 @@ struct MainArgs {
   int tau_fast;         // the same for the one-cell paths (NEE cells, one cell per lane)
   unsigned long long* exact_waves;  // counts 4-cell waves that fell back to the exact division
   const int* stopped;   // nullable
-  // NEE-adjacent fluid cells
-  const int* cells;     // linear ids
-  float4* prev;         // per cell: its (rho, ux, uy, uz) of the previous step
-  const float4* nee_bc;   // per cell, kNeeSlots records: the boundary data (rho_bc or NaN, u_bc)
-                          // of its first NEE directions -- static, so loaded with the cell id
-  const uint2* nee_mask;  // per cell: x bit q set when c - e_q is an NEE cell supplying q
-                          // (face match), y bit q when that cell is a pressure boundary
-  int n_nee;
-  int nee_blocks;       // multiple of 8 (keeps the chunk blocks' XCD order)
-  int nee_waves;        // active waves per NEE block (1 for short lists: a cell's loads are
-                        // scattered lines, so spreading the waves over more CUs' load pipes pays)
-  int nee_active;       // 0 at step 0: NEE cells are pulled raw (boundary_stream has not run)
   float omc;            // the reference's (1.0f - 1.0f / tau)
   int swap;             // 1: storage rows run along physical y (Layout::swap)
   // The previous step's residual inside this launch (single domain, one cell per lane, no
@@ -130,17 +119,8 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
-constexpr int kNeeSlots = 5;  // NEE directions per cell whose data is gathered (one flat face: 5)
-// nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of mask[i].x
-hipError_t launch_nee_gather(const int* cells, const uint2* mask, const float* rho, const float* ux,
-                             const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
-                             int swap, hipStream_t s);
 int main_grid(int nchunks, bool quarter);
 constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
-// 1 active wave per NEE block for short, scattered lists (contiguous = fraction of list
-// neighbours that are storage neighbours: their lanes share lines), else 4
-int nee_waves_for(int n, double contiguous);
-int nee_grid(int n, int waves);
 constexpr int kReduceBlocks = 256;
 // partial sums -> conv->s_local (deterministic: one block for up to 16384 partials, else
 // kReduceBlocks blocks sum fixed contiguous slices into scratch and one block sums those);
@@ -150,7 +130,6 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
                          double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
 // lazy macros: (rho, u) of the fluid cells in [lo, hi) from the last step's source buffer
-// (NEE-adjacent cells excepted), then those cells' kept (rho, u)
 hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
                           int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
 // per local plane digest of the fluid (rho, u) bits keyed by global coordinates (lbm_field_digest);
@@ -158,8 +137,6 @@ hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, flo
 hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux, const float* uy, const float* uz,
                          int nx, int ny, int nz, int pitch, int xshift, int64_t plane, int z_offset, int swap,
                          unsigned long long* out, hipStream_t s);
-hipError_t launch_prev_scatter(const int* cells, const float4* prev, int n, float* rho, float* ux, float* uy,
-                               float* uz, hipStream_t s);
 
 // streaming copy of n4 16-B vectors (lbm_probe_stream): `blocks` x 256 threads; shape 0/1
 // grid-stride non-temporal / plain, 2/3 the same with one contiguous region per XCD, 4/5
@@ -196,6 +173,7 @@ struct GeoArgs {
   const int8_t* codes;
   uint8_t* type;
   uint32_t* links;         // per cell wall-link masks (written for fluid cells)
+  uint32_t* nlinks;        // per cell NEE-link masks (written for fluid cells)
   float* rho; float* ux; float* uy; float* uz;  // NEE data written at NEE cells
   const float* inlet_uy;   // nx * nz_global (nullable)
   const float* outlet_uy;

@@ -34,7 +34,9 @@ struct orc_lbm {
     orc_bc bcs[16];                  /* ORC_GENERIC (tables owned) */
     int nbc;
     float sum_current;               /* ldc.cu:652 sum_current */
-    int residual_fp64;               /* 1: S summed in fp64 (liblbm's sum), not thrust's fp32 */
+    int residual_mode;               /* ORC_SUM_*: how S is summed (orc_set_residual_mode) */
+    int cub_ipt, cub_vec, cub_grid;  /* ORC_SUM_CUB_TREE: items per thread, vector width, grid cap */
+    float* terms;                    /* ORC_SUM_CUB_TREE: the |u| terms in reference storage order */
 };
 
 static inline long cidx(const orc_lbm* o, int x, int y, int z) {
@@ -449,7 +451,7 @@ void orc_destroy(orc_lbm* o) {
     for (int k = 0; k < o->nbc; k++) free((void*)o->bcs[k].table);
     free(o->geo); free(o->src); free(o->dst);
     free(o->rho); free(o->ux); free(o->uy); free(o->uz);
-    free(o->inlet_uy); free(o->outlet_uy);
+    free(o->inlet_uy); free(o->outlet_uy); free(o->terms);
     free(o);
 }
 
@@ -657,11 +659,135 @@ static void nee_pressure_cell(orc_lbm* o, int x, int y, int z) {
     }
 }
 
-/* thrust::reduce of calc_vel_square (ldc.cu:460-466, 660-662), emulated serially in fp32
- * over the reference storage order: LDC brick order (8x8x8, ldc.cu:71), otherwise the
- * compact z,y,x order of index_transform.  Cells never written hold 0. */
+/* calc_vel_square's terms (ldc.cu:460-466) in the reference storage order: LDC brick order
+ * over the brick-padded box (8x8x8, ldc.cu:71), otherwise the compact z,y,x order of
+ * index_transform (Poiseulle.cu:257-271).  Cells never written hold 0.  Returns the count. */
+static long velsum_terms(const orc_lbm* o, float* t) {
+    const int nx = o->nx, ny = o->ny, nz = o->nz;
+    long n = 0;
+    if (o->kind == ORC_LDC) {
+        int bx = 1 + (nx - 1) / 8, by = 1 + (ny - 1) / 8, bz = 1 + (nz - 1) / 8;
+        for (int b = 0; b < bx * by * bz; b++) {
+            int ix = b % bx, iy = (b / bx) % by, iz = b / (bx * by);
+            for (int k = 0; k < 8; k++)
+                for (int j = 0; j < 8; j++)
+                    for (int i = 0; i < 8; i++) {
+                        int x = ix * 8 + i, y = iy * 8 + j, z = iz * 8 + k;
+                        float v = 0.f;
+                        if (x < nx && y < ny && z < nz) {
+                            long c = cidx(o, x, y, z);
+                            float ux = o->ux[c], uy = o->uy[c], uz = o->uz[c];
+                            v = sqrtf(ux * ux + uy * uy + uz * uz);
+                        }
+                        t[n++] = v;
+                    }
+        }
+    } else {
+        for (long c = 0; c < o->ncell; c++) {
+            if (o->geo[c] == 0) continue;
+            float ux = o->ux[c], uy = o->uy[c], uz = o->uz[c];
+            t[n++] = sqrtf(ux * ux + uy * uy + uz * uz);
+        }
+    }
+    return n;
+}
+
+/* CUB-style device reduction of n fp32 terms (cub::DeviceReduce / thrust::reduce's two-pass
+ * scheme, restated from CUB's published algorithm; the reference's CUDA/CUB version and GPU
+ * fix its parameters, which it does not record, so they are arguments):
+ *  pass 1: grid = min(tiles, grid_cap) blocks of 256 threads over tiles of 256*ipt items,
+ *          "even share" (block b takes a contiguous run of tiles, the first tiles % grid
+ *          blocks one tile more).  In a full tile thread t loads vec-wide vectors at
+ *          4t + 256*vec*i (i < ipt/vec) and folds the ipt items serially into its running
+ *          sum (the first tile starts the sum with its first item); a partial tile is read
+ *          striped (t, t + 256, ...).  Block reduction: 32-lane warps reduce by shuffle-down
+ *          trees (offsets 1, 2, 4, 8, 16; lane l adds lane l + offset when that lane holds
+ *          data), then thread 0 adds the warp sums serially.
+ *  pass 2: one block over the grid partials (one per thread, striped), reduced the same way;
+ *          S = 0.f + that (thrust's init). */
+static float warp_tree(float* v, int valid) {   /* v[0..32): lane values; valid lanes hold data */
+    for (int off = 1; off < 32; off <<= 1)
+        for (int l = 0; l < 32; l++)             /* shuffle-down: reads of the previous round */
+            if (l + off < valid && (l % (2 * off)) == 0) v[l] = v[l + off] + v[l];
+    return v[0];
+}
+static float block_reduce(float* agg, int num_valid) {
+    float lane[32], s = 0.f;
+    for (int w = 0; w < 8; w++) {
+        int valid = num_valid - 32 * w;
+        if (valid <= 0) break;
+        if (valid > 32) valid = 32;
+        for (int l = 0; l < 32; l++) lane[l] = agg[32 * w + l];
+        float ws = warp_tree(lane, valid);
+        s = (w == 0) ? ws : s + ws;
+    }
+    return s;
+}
+float orc_cub_reduce(const float* v, long n, int ipt, int vec, int grid_cap) {
+    const long tile = 256L * ipt;
+    const long tiles = (n + tile - 1) / tile;
+    if (n <= 0) return 0.f;
+    long grid = tiles < grid_cap ? tiles : grid_cap;
+    if (tiles <= 1) grid = 1;
+    const long avg = tiles / grid, big = tiles - avg * grid;
+    float* part = (float*)malloc(sizeof(float) * (size_t)grid);
+    float agg[256];
+    for (long b = 0; b < grid; b++) {
+        long t0 = b < big ? b * (avg + 1) : big * (avg + 1) + (b - big) * avg;
+        long off = t0 * tile, end = off + (avg + (b < big)) * tile;
+        if (end > n) end = n;
+        int first = 1, num_valid = 256;
+        for (; off + tile <= end; off += tile, first = 0)
+            for (int t = 0; t < 256; t++) {
+                float s = first ? 0.f : agg[t];
+                int k0 = first;
+                if (first) s = v[off + (long)vec * t];
+                for (int i = 0; i < ipt / vec; i++)
+                    for (int k = 0; k < vec; k++) {
+                        if (k0) { k0 = 0; continue; }
+                        s = s + v[off + (long)vec * t + 256L * vec * i + k];
+                    }
+                agg[t] = s;
+            }
+        if (off < end) {  /* partial tile: striped */
+            long valid = end - off;
+            for (int t = 0; t < 256; t++) {
+                long i = t;
+                if (first) {
+                    if (i >= valid) continue;
+                    agg[t] = v[off + i];
+                    i += 256;
+                }
+                for (; i < valid; i += 256) agg[t] = agg[t] + v[off + i];
+            }
+            if (first) num_valid = valid < 256 ? (int)valid : 256;
+        }
+        part[b] = block_reduce(agg, num_valid);
+    }
+    float s;
+    if (grid == 1) s = part[0];
+    else {  /* pass 2: one partial tile of grid items */
+        long i;
+        for (int t = 0; t < 256; t++) {
+            i = t;
+            if (i >= grid) continue;
+            agg[t] = part[i];
+            for (i += 256; i < grid; i += 256) agg[t] = agg[t] + part[i];
+        }
+        s = block_reduce(agg, grid < 256 ? (int)grid : 256);
+    }
+    free(part);
+    return 0.f + s;
+}
+
+/* thrust::reduce of calc_vel_square (ldc.cu:460-466, 660-662): by default emulated serially
+ * in fp32 over the reference storage order (velsum_terms) */
 float orc_velsum(const orc_lbm* o) {
-    if (o->residual_fp64) {
+    if (o->residual_mode == ORC_SUM_CUB_TREE) {
+        long n = velsum_terms(o, o->terms);
+        return orc_cub_reduce(o->terms, n, o->cub_ipt, o->cub_vec, o->cub_grid);
+    }
+    if (o->residual_mode == ORC_SUM_FP64) {
         /* liblbm's S: the same fp32 |u| terms accumulated in fp64 over the stored cells (the
          * off-fluid ones hold 0), rounded to fp32 once -- an accurate summation, the limit
          * thrust's fp32 tree approaches; the reference's own order is unspecified */
@@ -812,7 +938,26 @@ void orc_set_f(orc_lbm* o, const float* f) {
 
 long orc_bad_reads(const orc_lbm* o) { return o->bad_reads; }
 
-void orc_set_residual_fp64(orc_lbm* o, int on) { o->residual_fp64 = on ? 1 : 0; }
+void orc_set_residual_fp64(orc_lbm* o, int on) { o->residual_mode = on ? ORC_SUM_FP64 : ORC_SUM_SERIAL; }
+
+int orc_set_residual_mode(orc_lbm* o, int mode, int ipt, int vec, int grid_cap) {
+    if (mode < ORC_SUM_SERIAL || mode > ORC_SUM_CUB_TREE) return -1;
+    if (mode == ORC_SUM_CUB_TREE) {
+        if (ipt < 1 || vec < 1 || ipt % vec || grid_cap < 1) return -1;
+        if (!o->terms) {
+            long cap = o->ncell + 8L * 8 * 8 * (o->nx / 8 + 2) * (o->ny / 8 + 2) * 2;  /* brick padding */
+            if (o->kind == ORC_LDC) {
+                long bx = 1 + (o->nx - 1) / 8, by = 1 + (o->ny - 1) / 8, bz = 1 + (o->nz - 1) / 8;
+                cap = bx * by * bz * 512;
+            }
+            o->terms = (float*)malloc(sizeof(float) * (size_t)cap);
+            if (!o->terms) return -1;
+        }
+        o->cub_ipt = ipt; o->cub_vec = vec; o->cub_grid = grid_cap;
+    }
+    o->residual_mode = mode;
+    return 0;
+}
 
 /* bifurcation.cu:1158-1175 */
 double orc_calc_res_bif(const orc_lbm* o) {

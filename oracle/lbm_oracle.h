@@ -106,6 +106,13 @@ float orc_velsum(const orc_lbm* o);
 /* residual sum mode: 0 (default) thrust's fp32 sum emulated serially in the reference storage
  * order; 1 the fp32 |u| terms summed in fp64 (liblbm's S), for stop-step comparisons */
 void orc_set_residual_fp64(orc_lbm* o, int on);
+/* residual sum modes (orc_set_residual_mode) */
+enum { ORC_SUM_SERIAL = 0, ORC_SUM_FP64 = 1, ORC_SUM_CUB_TREE = 2 };
+/* ORC_SUM_CUB_TREE: thrust::reduce's CUB two-pass fp32 tree over the terms in reference storage
+ * order, with 256-thread blocks, ipt items per thread loaded vec wide, at most grid_cap blocks
+ * (see orc_cub_reduce); returns 0, or -1 for bad parameters */
+int orc_set_residual_mode(orc_lbm* o, int mode, int ipt, int vec, int grid_cap);
+float orc_cub_reduce(const float* v, long n, int ipt, int vec, int grid_cap);
 
 #ifdef __cplusplus
 }

@@ -66,6 +66,8 @@ def lib() -> C.CDLL:
             "orc_calc_res_bif": (C.c_double, [P]),
             "orc_velsum": (C.c_float, [P]),
             "orc_set_residual_fp64": (None, [P, C.c_int]),
+            "orc_set_residual_mode": (C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
+            "orc_cub_reduce": (C.c_float, [f32p, C.c_long, C.c_int, C.c_int, C.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -235,6 +237,20 @@ class Oracle:
     def residual_fp64(self, on: bool = True) -> None:
         """Sum |u| in fp64 like liblbm (default: thrust's fp32 sum, serial, storage order)."""
         lib().orc_set_residual_fp64(self.h, 1 if on else 0)
+
+    def residual_cub_tree(self, ipt: int = 16, vec: int = 4, grid_cap: int = 240) -> None:
+        """Sum |u| with thrust::reduce's CUB two-pass fp32 tree (orc_cub_reduce)."""
+        if lib().orc_set_residual_mode(self.h, SUM_CUB_TREE, ipt, vec, grid_cap) != 0:
+            raise ValueError(f"bad CUB tree parameters ipt={ipt} vec={vec} grid_cap={grid_cap}")
+
+
+SUM_SERIAL, SUM_FP64, SUM_CUB_TREE = 0, 1, 2
+
+
+def cub_reduce(v: np.ndarray, ipt: int = 16, vec: int = 4, grid_cap: int = 240) -> float:
+    """orc_cub_reduce over a float32 array (the emulated CUB two-pass tree)."""
+    v = np.ascontiguousarray(v, np.float32)
+    return float(lib().orc_cub_reduce(_p(v, C.c_float), v.size, ipt, vec, grid_cap))
 
 
 def feq(rho: float, ux: float, uy: float, uz: float) -> np.ndarray:
