@@ -196,6 +196,22 @@ int lbm_init_case(lbm_ctx* ctx);
 /* Exact initial populations, SoA [19][nz][ny][nx] (into both buffers); resets the step count. */
 int lbm_set_f(lbm_ctx* ctx, const float* f_soa);
 
+/* Summation order of the residual's S = sum |u| (ldc.cu:460-466, 660-668).  The reference sums
+ * the fp32 terms with thrust::reduce, CUB's two-pass device reduction, whose tree shape depends
+ * on its CUDA/CUB version and GPU (not recorded by the reference); the stop step of a
+ * convergence-controlled run depends on that order (oracle/PINNING.md section 3).
+ *   LBM_SUM_FP64 (default): the fp32 terms summed in fp64 in a fixed order -- no slower than the
+ *     step itself (the sum rides in the next step's launch).
+ *   LBM_SUM_CUB_TREE: the terms in the reference's storage order (LDC: 8x8x8 bricks over the
+ *     brick-padded box, ldc.cu:71; otherwise index_transform's compact z, y, x order), summed in
+ *     fp32 by CUB's tree: blocks of 256 threads, items_per_thread items per thread loaded vec
+ *     wide (a multiple), at most grid_cap blocks (e.g. 16, 4, 240: CUB's sm_60 policy on the
+ *     thesis's 6-SM GTX 1050 Ti), 32-lane warp shuffle trees -- bit-identical to the oracle's
+ *     orc_cub_reduce.  Two extra launches per step (one re-reads the step's populations).
+ * Single-domain contexts only (LBM_ERR_ARG otherwise); vec and grid_cap are ignored for FP64. */
+typedef enum { LBM_SUM_FP64 = 0, LBM_SUM_CUB_TREE = 1 } lbm_sum_order;
+int lbm_set_residual_order(lbm_ctx* ctx, int mode, int items_per_thread, int vec, int grid_cap);
+
 /* Convergence control of the reference main loop (ldc.cu:653-685): when enabled, a device
  * flag stops stepping once !(k <= max_it && tol_count <= stag_max); further steps are no-ops. */
 int lbm_set_convergence(lbm_ctx* ctx, int enabled, int max_it, int stag_max, float tol);

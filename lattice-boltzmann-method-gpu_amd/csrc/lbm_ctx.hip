@@ -56,8 +56,13 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int* chunks = nullptr;  // active 256-cell chunks (>= 1 fluid cell in range)
   int chunk0 = -1;        // >= 0: chunks is chunk0, chunk0 + 1, ... (the kernel skips the list)
   int nchunks = 0;
+  // 4-cell ranges: NEE-adjacent fluid cells, one per thread in the NEE blocks
+  int* cells = nullptr;
+  uint32_t* cell_nl = nullptr;  // their NEE-link masks
+  float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
+  int n_nee = 0, nee_blocks = 0, nee_waves = 4;
   unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
-  double* part = nullptr; // one |u| partial per chunk block
+  double* part = nullptr; // one |u| partial per block (NEE blocks, then chunk blocks)
   int npart = 0;
   int main_blocks = 0;
   bool stride = false;    // grid-stride chunk loop (LBM_TUNE_GRID_STRIDE)
@@ -125,6 +130,14 @@ struct lbm_ctx {
   // and the residual are stale from then on, so every later step, wait and read-out fails with
   // LBM_ERR_RCCL instead of silently running the slab as a single domain
   bool comm_failed = false;
+  // residual summation order (lbm_set_residual_order): LBM_SUM_FP64, or the reference-order
+  // fp32 CUB tree over n_ref terms (ref_idx: reference storage slot per fluid cell, -1 else)
+  int sum_mode = LBM_SUM_FP64;
+  int cub_ipt = 16, cub_vec = 4, cub_grid = 240;
+  int* ref_idx = nullptr;
+  float* terms = nullptr;
+  float* cub_part = nullptr;
+  int64_t n_ref = 0;
   std::string err;
 };
 
@@ -310,6 +323,8 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
+  a.cells = r.cells; a.cell_nl = r.cell_nl; a.nee_bc = r.nee_bc; a.n_nee = r.n_nee;
+  a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
   if (fr) {
     a.partial = fr->part;
     a.red_blocks = 8;
@@ -318,7 +333,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
     a.red_conv = c->conv;
     a.red_hist = fr->hist;
   }
-  if (r.main_blocks > 0 || fr) {
+  if (r.main_blocks + r.nee_blocks > 0 || fr) {
     c->launches++;
     RCK(timed(c, st, kKindStep, kKindSrc0 + srcbuf, range_kind, [&] {
                 HIPCK(c, launch_step(a, st));
@@ -337,7 +352,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   r.c_hi = hi;
   r.c_lo2 = lo2;
   r.c_hi2 = hi2;
-  std::vector<int> chunks;
+  std::vector<int> chunks, cells;
   auto in = [&](int64_t k) { return (k >= lo && k < hi) || (k >= lo2 && k < hi2); };
   auto scan = [&](int64_t a, int64_t b) {
     for (int64_t ch = a / kChunk; ch * kChunk < b; ++ch) {
@@ -348,6 +363,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         const uint8_t v = t[k];
         if ((v & kClassMask) != kFluid) continue;
         any = true;
+        if (v & kNeeAdj) cells.push_back((int)k);
       }
       if (any) chunks.push_back((int)ch);
     }
@@ -366,8 +382,57 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     const int cpl = g_tune[LBM_TUNE_CELLS_PER_LANE];  // A/B switch: 1 or 4 (0: by size)
     r.quarter = cpl ? (cpl == 1) : (r.nchunks <= kQuarterMaxChunks);
   }
+  // 4-cell ranges: the NEE-adjacent cells go to NEE blocks, one per thread.  In a chunk wave
+  // each would add two dependent load rounds (its NEE-link mask, then its neighbours' boundary
+  // data) to the whole wave -- on the pipe with rows along y, to every wave.  One-cell waves
+  // load the link mask with the pulls and keep them (the boundary data arrives under the
+  // arithmetic).
+  double contig = 1.0;
+  if (r.quarter) cells.clear();
+  r.n_nee = (int)cells.size();
+  if (r.n_nee) {
+    std::vector<uint32_t> nl(cells.size());
+    {  // the NEE-link masks of k_flag_fluid: q crosses the NEE neighbour's face (e_q . n == 1)
+      int64_t off[kQ];
+      for (int q = 0; q < kQ; ++q) {
+        const int s0 = c->L.swap ? kEy[q] : kEx[q], s1 = c->L.swap ? kEx[q] : kEy[q];
+        off[q] = s0 + (int64_t)s1 * c->L.pitch + (int64_t)kEz[q] * c->L.plane;
+      }
+      for (size_t i = 0; i < cells.size(); ++i)
+        for (int q = 1; q < kQ; ++q) {
+          const int64_t nb = cells[i] - off[q];
+          if (nb < 0 || nb >= (int64_t)t.size() || (t[nb] & kClassMask) != kNee) continue;
+          const int fb = (kEx[q] == 1 ? 1 : 0) | (kEx[q] == -1 ? 2 : 0) | (kEy[q] == 1 ? 4 : 0) |
+                         (kEy[q] == -1 ? 8 : 0) | (kEz[q] == 1 ? 16 : 0) | (kEz[q] == -1 ? 32 : 0);
+          if ((fb >> nee_face(t[nb])) & 1) nl[i] |= 1u << q;
+        }
+    }
+    // group cells with the same directions (inlet / outlet / lid faces, edges) so that the
+    // lanes of a wave take the same branches; cell order within a group
+    std::vector<size_t> perm(cells.size());
+    for (size_t i = 0; i < perm.size(); ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](size_t x, size_t y) { return nl[x] < nl[y]; });
+    std::vector<int> sc(cells.size());
+    std::vector<uint32_t> snl(cells.size());
+    for (size_t i = 0; i < perm.size(); ++i) {
+      sc[i] = cells[perm[i]];
+      snl[i] = nl[perm[i]];
+    }
+    int64_t adj = 0;  // list neighbours that are storage neighbours (their lanes share lines)
+    for (size_t i = 1; i < sc.size(); ++i) adj += sc[i] == sc[i - 1] + 1;
+    if (sc.size() > 1) contig = (double)adj / (double)(sc.size() - 1);
+    HIPCK(c, hipMalloc(&r.cells, sizeof(int) * r.n_nee));
+    HIPCK(c, hipMemcpy(r.cells, sc.data(), sizeof(int) * r.n_nee, hipMemcpyHostToDevice));
+    HIPCK(c, hipMalloc(&r.cell_nl, sizeof(uint32_t) * r.n_nee));
+    HIPCK(c, hipMemcpy(r.cell_nl, snl.data(), sizeof(uint32_t) * r.n_nee, hipMemcpyHostToDevice));
+    // the boundary cells' data is written by classification and never changes afterwards
+    HIPCK(c, hipMalloc(&r.nee_bc, sizeof(float4) * kNeeSlots * r.n_nee));
+    HIPCK(c, launch_nee_gather(r.cells, r.cell_nl, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.n_nee, c->L.pitch,
+                               c->L.plane, c->L.swap, c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+  }
   // Lane masks for the 4-cell path: bit l of a chunk's mask is set when lane l (cells 4l ..
-  // 4l+3) holds a cell the chunk wave updates (fluid, in range) or neighbours
+  // 4l+3) holds a cell the chunk wave updates (fluid, in range, not NEE-adjacent) or neighbours
   // such a lane (the DPP x-shift reads the next lanes' slices).  Lanes outside it load nothing:
   // on a vessel tree most chunks are partly empty (the upsampled bifurcation keeps 51% of its
   // active chunks' cells).  Only for sparse chunk lists, whose waves load their chunk id
@@ -383,7 +448,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         for (int k = 0; k < 4; ++k) {
           const int64_t cell = base + 4 * l + k;
           const uint8_t v = t[cell];
-          if (in(cell) && (v & kClassMask) == kFluid) m |= 1ull << l;
+          if (in(cell) && (v & kClassMask) == kFluid && !(v & kNeeAdj)) m |= 1ull << l;
         }
       busy += __builtin_popcountll(m);
       m |= (m << 1) | (m >> 1);
@@ -413,13 +478,18 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       r.stride = true;
     }
   }
-  r.npart = r.main_blocks;
+  r.nee_waves = nee_waves_for(r.n_nee, contig);
+  r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);
+  r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }
 
 void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.lane_masks) (void)hipFree(r.lane_masks);
+  if (r.cells) (void)hipFree(r.cells);
+  if (r.cell_nl) (void)hipFree(r.cell_nl);
+  if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
 }
 
@@ -805,6 +875,9 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->conv) (void)hipFree(c->conv);
   if (c->retried) (void)hipFree(c->retried);
   if (c->qsets) (void)hipFree(c->qsets);
+  if (c->ref_idx) (void)hipFree(c->ref_idx);
+  if (c->terms) (void)hipFree(c->terms);
+  if (c->cub_part) (void)hipFree(c->cub_part);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->ev_edge, c->ev_halo, c->ev_sum, c->ev_fin})
     if (e) (void)hipEventDestroy(e);
@@ -898,6 +971,69 @@ int lbm_get_numerics(lbm_ctx* c, int* fast_div, int64_t* retried_chunks) {
   return LBM_OK;
 }
 
+int lbm_set_residual_order(lbm_ctx* c, int mode, int items_per_thread, int vec, int grid_cap) {
+  if (!c) return LBM_ERR_ARG;
+  if (mode == LBM_SUM_FP64) {
+    c->sum_mode = mode;
+    return LBM_OK;
+  }
+  if (mode != LBM_SUM_CUB_TREE || items_per_thread < 1 || vec < 1 || items_per_thread % vec || grid_cap < 1 ||
+      grid_cap > 65536) {
+    c->err = "lbm_set_residual_order: mode LBM_SUM_FP64 or LBM_SUM_CUB_TREE with items_per_thread a multiple of "
+             "vec and 1 <= grid_cap <= 65536";
+    return LBM_ERR_ARG;
+  }
+  if (c->comm || c->d.nz_global != c->d.nz) {
+    c->err = "lbm_set_residual_order: the reference-order sum is defined for a single-domain lattice only";
+    return LBM_ERR_ARG;
+  }
+  HIPCK(c, hipSetDevice(c->d.device));
+  if (!c->ref_idx) {
+    // reference storage order: LDC bricks of 8 x 8 x 8 over the brick-padded box (ldc.cu:71),
+    // otherwise index_transform's compact z, y, x order of the stored cells (code != 0,
+    // Poiseulle.cu:257-271, bifurcation.cu:241-252); the fluid cells' slots get their |u|
+    const Layout& L = c->L;
+    std::vector<uint8_t> t((size_t)L.ncell);
+    std::vector<int8_t> codes((size_t)L.ncell);
+    HIPCK(c, hipMemcpy(t.data(), c->type, L.ncell, hipMemcpyDeviceToHost));
+    HIPCK(c, hipMemcpy(codes.data(), c->codes, L.ncell, hipMemcpyDeviceToHost));
+    std::vector<int> ri((size_t)L.ncell, -1);
+    const bool ldc = c->d.case_kind == LBM_CASE_LDC;
+    const int64_t bx = (L.nx + 7) / 8, by = (L.ny + 7) / 8, bz = (L.nz + 7) / 8;
+    int64_t n = ldc ? bx * by * bz * 512 : 0;
+    for (int z = 0; z < L.nz; ++z)
+      for (int y = 0; y < L.ny; ++y)
+        for (int x = 0; x < L.nx; ++x) {
+          const int64_t s = cell_of(L, x, y, z);
+          int64_t r;
+          if (ldc) {
+            r = ((x / 8) + (y / 8) * bx + (z / 8) * bx * by) * 512 + x % 8 + (y % 8) * 8 + (z % 8) * 64;
+          } else {
+            if (codes[s] == 0) continue;
+            r = n++;
+          }
+          if ((t[s] & kClassMask) == kFluid) ri[s] = (int)r;
+        }
+    if (n >= ((int64_t)1 << 31)) {
+      c->err = "lbm_set_residual_order: lattice too large for 32-bit reference indices";
+      return LBM_ERR_ARG;
+    }
+    c->n_ref = n;
+    HIPCK(c, hipMalloc(&c->ref_idx, sizeof(int) * L.ncell));
+    HIPCK(c, hipMemcpy(c->ref_idx, ri.data(), sizeof(int) * L.ncell, hipMemcpyHostToDevice));
+    HIPCK(c, hipMalloc(&c->terms, sizeof(float) * std::max<int64_t>(1, n)));
+    HIPCK(c, hipMemset(c->terms, 0, sizeof(float) * std::max<int64_t>(1, n)));
+  }
+  if (c->cub_part) HIPCK(c, hipFree(c->cub_part));
+  c->cub_part = nullptr;
+  HIPCK(c, hipMalloc(&c->cub_part, sizeof(float) * cub_grid(c->n_ref, items_per_thread, grid_cap)));
+  c->cub_ipt = items_per_thread;
+  c->cub_vec = vec;
+  c->cub_grid = grid_cap;
+  c->sum_mode = mode;
+  return LBM_OK;
+}
+
 int lbm_set_convergence(lbm_ctx* c, int enabled, int max_it, int stag_max, float tol) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
@@ -981,6 +1117,20 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
 }
 
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
+  if (c->sum_mode == LBM_SUM_CUB_TREE) {
+    // the reference's order: per step calc_vel_square's terms into reference storage order, then
+    // thrust::reduce's CUB tree in fp32 (ldc.cu:660-668)
+    const Layout& L = c->L;
+    for (int s = 0; s < nsteps; ++s) {
+      RCK(run_range(c, c->whole, c->cur, c->s_comp));
+      HIPCK(c, launch_vel_terms(c->buf[c->cur], c->type, c->ref_idx, c->terms, L.plane, (L.nz + 1) * L.plane, L.pitch,
+                                L.plane, L.swap, c->s_comp));
+      c->cur ^= 1;
+      HIPCK(c, launch_cub_tree(c->terms, c->n_ref, c->cub_ipt, c->cub_vec, c->cub_grid, c->cub_part, c->conv,
+                               want_hist ? c->hist + s : nullptr, c->s_comp));
+    }
+    return LBM_OK;
+  }
   if (c->fuse_red && !c->conv_enabled) {
     // one launch per step: step s's k_step also finishes step s-1's residual; the last
     // step's own reduction follows the loop
@@ -1558,6 +1708,10 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
   HIPCK(c, hipSetDevice(c->d.device));
   ncclUniqueId id;
   std::memcpy(&id, id_bytes, 128);
+  if (c->sum_mode != LBM_SUM_FP64) {
+    c->err = "lbm_attach_rccl: the reference-order residual (lbm_set_residual_order) is single-domain only";
+    return LBM_ERR_ARG;
+  }
   NCCK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
   c->nranks = nranks;
@@ -1612,7 +1766,8 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   for (int i = 0; i < n; ++i) {
     if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xshift != c0->L.xshift ||
         cs[i]->L.swap != c0->L.swap || cs[i]->L.plane != c0->L.plane ||
-        cs[i]->steps_done != c0->steps_done || cs[i]->cur != c0->cur || cs[i]->conv_enabled || cs[i]->comm) {
+        cs[i]->steps_done != c0->steps_done || cs[i]->cur != c0->cur || cs[i]->conv_enabled || cs[i]->comm ||
+        cs[i]->sum_mode != LBM_SUM_FP64) {
       c0->err = "lbm_group_step: slabs must share device, row layout (nx, ny, x_align) and step count, "
                 "without convergence control or RCCL";
       return LBM_ERR_ARG;

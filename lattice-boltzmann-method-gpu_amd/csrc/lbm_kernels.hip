@@ -255,10 +255,6 @@ __device__ __forceinline__ int64_t cell_off_rt(int q, int pitch, int64_t plane) 
   return (SW ? ey : ex) + (int64_t)(SW ? ex : ey) * pitch + (int64_t)ez * plane;
 }
 
-// NEE directions of a cell whose boundary data is loaded ahead (one flat face: 5); a cell
-// with more (edges and corners of several faces) loads the rest where they are used
-constexpr int kNeeSlots = 5;
-
 __device__ __forceinline__ float4 bc_at(const MainArgs& a, int64_t b) {
   return make_float4(a.rho[b], a.ux[b], a.uy[b], a.uz[b]);
 }
@@ -302,10 +298,7 @@ __device__ __forceinline__ float nee_value(float fq, float4 b, float r, float ux
   return e_bc + (fq - e_nb) * omc;
 }
 
-// the cell's post-collision f_Q, for nee_store_q:
-//  Post1: one cell in registers after its relaxation;
-//  Pre4:  cell j of a 4-cell lane before the relaxation -- f_Q relaxed here by the same
-//         expression as relax_cell (fast: the 3-VALU quotient), so the bits agree
+// the cell's post-collision f_Q, for nee_store_q: one cell in registers after its relaxation
 struct Post1 {
   const float* f;
   template <int Q>
@@ -313,23 +306,6 @@ struct Post1 {
     return f[Q];
   }
 };
-__device__ __forceinline__ float sel4(f4 v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
-struct Pre4 {
-  const f4* v;
-  int j;
-  bool fast;
-  template <int Q>
-  __device__ __forceinline__ float post(const MainArgs& a, float r, float ux, float uy, float uz) const {
-    const float f = sel4(v[Q], j);
-    const float x = f - feq<Q>(r, ux, uy, uz);
-    if (fast) {
-      const float q0 = x * a.tau_rcp;
-      return f - __builtin_fmaf(__builtin_fmaf(-q0, a.tau, x), a.tau_rcp, q0);
-    }
-    return f - x / a.tau;
-  }
-};
-
 template <int Q, bool SW, class Src>
 __device__ __forceinline__ void nee_store_q(const MainArgs& a, int64_t c, uint32_t nl, float4 b0, float4 b1, float4 b2,
                                             float4 b3, float4 b4, const Src& src, float r, float ux, float uy,
@@ -374,20 +350,15 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   pull4_all<SW>(v, a.src, cb, c, lane, a.pitch, a.plane, need, AllQ{});
   const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
   const unsigned t4 = need ? t4r : 0u;
-  // wall- and NEE-link masks of the lane's boundary-adjacent cells (a dependent load, rare)
+  // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
+  // so this dependent load hides behind the arithmetic)
   constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
-  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
   if (t4 & kWall4) {
     if (t4 & (kWallAdj << 0)) m0 = a.links[c + 0];
     if (t4 & (kWallAdj << 8)) m1 = a.links[c + 1];
     if (t4 & (kWallAdj << 16)) m2 = a.links[c + 2];
     if (t4 & (kWallAdj << 24)) m3 = a.links[c + 3];
-  }
-  if (t4 & kNee4) {
-    if (t4 & (kNeeAdj << 0)) n0 = a.nlinks[c + 0];
-    if (t4 & (kNeeAdj << 8)) n1 = a.nlinks[c + 1];
-    if (t4 & (kNeeAdj << 16)) n2 = a.nlinks[c + 2];
-    if (t4 & (kNeeAdj << 24)) n3 = a.nlinks[c + 3];
   }
   float r0, r1, r2, r3, x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
   moments<0>(v, r0, x0, y0, z0);
@@ -413,7 +384,9 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   for (int j = 0; j < 4; ++j) {
     const unsigned t = (t4 >> (8 * j)) & 0xffu;
     const int64_t cj = c + j;
-    const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid;
+    // NEE-adjacent cells belong to the NEE blocks of the launch (nee_cell)
+    const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
+                    !(t & kNeeAdj);
     if (in) {
       store |= 1u << j;
       acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
@@ -421,32 +394,15 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
   // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
-  // bounce-back slots / boundary data and cells outside the launch's ranges belong to another
-  // launch, so those lanes store cell by cell -- sub-16-B stores cost whole partial-line
-  // writes in HBM (the x-ends of every row took 15% of the step before the xshift alignment).
+  // bounce-back slots / NEE values, and NEE-adjacent cells and cells outside the launch's
+  // ranges are stored by other threads, so those lanes store cell by cell -- sub-16-B stores
+  // cost whole partial-line writes in HBM (the x-ends of every row took 15% of the step before
+  // the xshift alignment).
   const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
   const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
-  const bool keep_others = special != 0u || !lane_in;
+  const bool keep_others = special != 0u || !lane_in || (t4 & kNee4);
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
-  // NEE values of the lane's NEE-adjacent cells (rare, divergent), before the relaxation so
-  // that the moments need not outlive it: cell j's f_q is relaxed once more here by the same
-  // expression.  One cell at a time keeps one copy of the 18-direction code and few registers.
-  if (t4 & kNee4) {
-    unsigned nee = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (((store >> j) & 1u) && ((t4 >> (8 * j)) & kNeeAdj)) nee |= 1u << j;
-    const f4 RH{r0, r1, r2, r3};
-#pragma unroll 1
-    for (; nee; nee &= nee - 1u) {
-      const int j = __builtin_ctz(nee);
-      const uint32_t nl = j == 0 ? n0 : j == 1 ? n1 : j == 2 ? n2 : n3;
-      const BcSlots bc = nee_prefetch<SW>(a, c + j, nl);
-      nee_store_all<SW>(a, c + j, nl, bc, Pre4{v, j, FAST && fast_wave}, sel4(RH, j), sel4(UX, j), sel4(UY, j),
-                        sel4(UZ, j), AllQ{});
-    }
-  }
   if (FAST && fast_wave) {
     relax_cell<0, true>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
     relax_cell<1, true>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
@@ -573,6 +529,32 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, i
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
+// One NEE-adjacent fluid cell of a 4-cell range (NEE blocks, one per thread; the chunk waves
+// leave these cells alone): every static datum -- the cell id, its NEE-link mask, the boundary
+// data of its first kNeeSlots NEE neighbours -- is indexed by the list position, so it all
+// goes out in one round trip, then the 19 plain pulls and the wall links.  Collide, store the
+// cell's slots, its bounce-back slots and its NEE neighbours' slots (producer side).
+template <bool SW>
+__device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
+  const int64_t c = a.cells[i];
+  const uint32_t nl = a.cell_nl[i];
+  const float4* r = a.nee_bc + (int64_t)i * kNeeSlots;
+  const BcSlots bc{r[0], r[1], r[2], r[3], r[4]};
+  const uint32_t links = a.links[c];
+  float f[kQ];
+  pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
+  float rho = 0.f;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) rho = rho + f[q];
+  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
+  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
+  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
+  relax1(f, a, rho, ux, uy, uz);
+  nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, AllQ{});
+  fix_store_all<SW>(f, a.dst, c, links, a.pitch, a.plane, AllQ{});
+  return (double)sqrtf(ux * ux + uy * uy + uz * uz);
+}
+
 // ---- the step kernel -------------------------------------------------------------------
 
 __device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {
@@ -617,13 +599,13 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       }
       __syncthreads();  // red[] reuse below
     }
-  } else {
+  } else if (bx >= a.nee_blocks) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own
     // L2), so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of
     // chunks and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
-    const int b = bx;  // red_blocks is a multiple of 8
+    const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
     if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
@@ -641,7 +623,14 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
       acc = process_chunk<FAST, SW, MASK>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base
     }
-    slot += a.red_blocks;
+    slot += a.red_blocks + a.nee_blocks;
+  } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
+    slot = blockIdx.x;
+    if constexpr (!QUARTER) {  // one-cell ranges have no NEE blocks
+      const int w = (int)threadIdx.x >> 6;
+      const int i = (bx * a.nee_waves + w) * 64 + ((int)threadIdx.x & 63);
+      if (w < a.nee_waves && i < a.n_nee) acc = nee_cell<SW>(a, i);
+    }
   }
   const double s = block_sum(acc, red);
   if (threadIdx.x == 0) a.partial[slot] = s;
@@ -1069,6 +1058,107 @@ __global__ void k_moments(const float* __restrict__ src, const uint8_t* __restri
   }
 }
 
+// ---- reference-order fp32 residual (opt-in) -----------------------------------------------
+// calc_vel_square (ldc.cu:460-466): the step's |u| per fluid cell -- from the step's source
+// buffer, the same pulls and sums as the step (k_moments) -- into its reference storage slot
+template <bool SW>
+__global__ void k_vel_terms(const float* __restrict__ src, const uint8_t* __restrict__ type,
+                            const int* __restrict__ ref_idx, float* __restrict__ terms, int64_t lo, int64_t hi,
+                            int pitch, int64_t plane) {
+  for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
+    if ((type[c] & kClassMask) != kFluid) continue;
+    float f[kQ];
+    pull1_all<SW>(f, src, c, pitch, plane, AllQ{});
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) r = r + f[q];
+    const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / r;
+    const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / r;
+    const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / r;
+    terms[ref_idx[c]] = sqrtf(ux * ux + uy * uy + uz * uz);
+  }
+}
+
+// CUB's block reduction (BLOCK_REDUCE_WARP_REDUCTIONS) with 32-lane logical warps on the
+// 64-lane wavefront: a shuffle-down tree per warp (offsets 1 .. 16; a lane adds its partner's
+// value only when the partner holds data), then thread 0 adds the warp sums in warp order.
+// num_valid: threads holding data (a prefix of the block).  Result valid in thread 0.
+__device__ float cub_block_sum(float x, int num_valid, float* warp_sums) {
+  const int t = threadIdx.x, w = t >> 5, l = t & 31;
+  const int valid = min(32, max(0, num_valid - 32 * w));
+#pragma unroll
+  for (int off = 1; off < 32; off <<= 1) {
+    const float y = __shfl_down(x, off, 32);
+    if (l + off < valid) x = y + x;
+  }
+  if (l == 0) warp_sums[w] = x;
+  __syncthreads();
+  float s = 0.f;
+  if (t == 0) {
+    s = warp_sums[0];
+    for (int k = 1; k < 8; ++k)
+      if (32 * k < num_valid) s = s + warp_sums[k];
+  }
+  return s;
+}
+
+// pass 1 (AgentReduce over an even share of tiles): in a full tile thread t folds the vec-wide
+// vectors at vec * t + 256 * vec * i, in a partial tile t, t + 256, ...
+__global__ __launch_bounds__(256) void k_cub_pass1(const float* __restrict__ v, int64_t n, int ipt, int vec,
+                                                   float* __restrict__ partials, const ConvState* cv) {
+  __shared__ float warp_sums[8];
+  if (cv->stopped) return;
+  const int64_t tile = 256LL * ipt;
+  const int64_t tiles = (n + tile - 1) / tile;
+  const int64_t grid = gridDim.x, b = blockIdx.x;
+  const int64_t avg = tiles / grid, big = tiles - avg * grid;
+  const int64_t t0 = b < big ? b * (avg + 1) : big * (avg + 1) + (b - big) * avg;
+  int64_t off = t0 * tile, end = off + (avg + (b < big ? 1 : 0)) * tile;
+  if (end > n) end = n;
+  const int t = threadIdx.x;
+  float x = 0.f;
+  bool have = false;
+  int num_valid = 256;
+  for (; off + tile <= end; off += tile)
+    for (int i = 0; i < ipt / vec; ++i)
+      for (int k = 0; k < vec; ++k) {
+        const float y = v[off + (int64_t)vec * t + 256LL * vec * i + k];
+        x = have ? x + y : y;
+        have = true;
+      }
+  if (off < end) {
+    const int64_t valid = end - off;
+    if (!have) num_valid = valid < 256 ? (int)valid : 256;
+    for (int64_t i = t; i < valid; i += 256) {
+      const float y = v[off + i];
+      x = have ? x + y : y;
+      have = true;
+    }
+  }
+  const float s = cub_block_sum(x, num_valid, warp_sums);
+  if (t == 0) partials[b] = s;
+}
+
+// pass 2 (the single-tile kernel over the partials) + the residual logic on S = 0.f + sum
+__global__ __launch_bounds__(256) void k_cub_pass2(const float* __restrict__ partials, int grid, ConvState* cv,
+                                                   float* hist_slot) {
+  __shared__ float warp_sums[8];
+  if (cv->stopped) return;
+  const int t = threadIdx.x;
+  float x = 0.f;
+  bool have = false;
+  for (int i = t; i < grid; i += 256) {
+    x = have ? x + partials[i] : partials[i];
+    have = true;
+  }
+  const float s = cub_block_sum(x, grid < 256 ? grid : 256, warp_sums);
+  if (t == 0) {
+    const float S = 0.f + s;  // thrust::reduce's init value
+    cv->s_local = (double)S;
+    residual_logic(cv, (double)S, hist_slot);
+  }
+}
+
 // ---- field digest ------------------------------------------------------------------------
 // Per local plane: the wrapping 64-bit sum over its fluid cells of a hash of (global x, y, z,
 // the bits of rho, ux, uy, uz).  Addition mod 2^64 is order-free, so the digest depends on
@@ -1138,10 +1228,14 @@ int main_grid(int nchunks, bool quarter) {
   return nchunks ? std::max(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
 }
 
+// NEE blocks of k_step (first in the grid): a multiple of 8 so the chunk blocks keep their XCD
+int nee_waves_for(int n, double contiguous) { return (n <= 16384 && contiguous < 0.5) ? 1 : kBlock / 64; }
+int nee_grid(int n, int waves) { return (n + 8 * 64 * waves - 1) / (8 * 64 * waves) * 8; }
+
 // Two waves per SIMD measured fastest (3.71 vs 3.83 ms at 512^3 with three, 5.2+ with one);
 // the 4-cell kernel's register count (214 VGPRs, kernel-resource-usage) gives exactly that.
 hipError_t launch_step(const MainArgs& a, hipStream_t s) {
-  const dim3 grid(a.red_blocks + a.main_blocks);
+  const dim3 grid(a.red_blocks + a.nee_blocks + a.main_blocks);
   typedef void (*Kern)(const MainArgs);
   const bool sw = a.swap != 0;
   Kern k;
@@ -1285,12 +1379,65 @@ hipError_t launch_probe_fill(void* dst, int64_t n4, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <bool SW>
+__global__ void k_nee_gather(const int* __restrict__ cells, const uint32_t* __restrict__ nl,
+                             const float* __restrict__ rho, const float* __restrict__ ux,
+                             const float* __restrict__ uy, const float* __restrict__ uz, float4* __restrict__ out,
+                             int n, int pitch, int64_t plane) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = cells[i];
+  uint32_t rest = nl[i];
+  for (int j = 0; j < kNeeSlots; ++j) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rest) {
+      const int q = __builtin_ctz(rest);
+      rest &= rest - 1u;
+      const int64_t b = c - cell_off_rt<SW>(q, pitch, plane);
+      v = make_float4(rho[b], ux[b], uy[b], uz[b]);
+    }
+    out[(int64_t)i * kNeeSlots + j] = v;
+  }
+}
+
+hipError_t launch_nee_gather(const int* cells, const uint32_t* nl, const float* rho, const float* ux,
+                             const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
+                             int swap, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g((n + 255) / 256);
+  if (swap) hipLaunchKernelGGL(k_nee_gather<true>, g, dim3(256), 0, s, cells, nl, rho, ux, uy, uz, nee_bc, n, pitch, plane);
+  else hipLaunchKernelGGL(k_nee_gather<false>, g, dim3(256), 0, s, cells, nl, rho, ux, uy, uz, nee_bc, n, pitch, plane);
+  return hipGetLastError();
+}
+
 hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
                           int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
   if (hi <= lo) return hipSuccess;
   const dim3 g(grid_for(hi - lo, 256));
   if (swap) hipLaunchKernelGGL(k_moments<true>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
   else hipLaunchKernelGGL(k_moments<false>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
+  return hipGetLastError();
+}
+
+hipError_t launch_vel_terms(const float* src, const uint8_t* type, const int* ref_idx, float* terms, int64_t lo,
+                            int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
+  if (hi <= lo) return hipSuccess;
+  const dim3 g(grid_for(hi - lo, 256));
+  if (swap) hipLaunchKernelGGL(k_vel_terms<true>, g, dim3(256), 0, s, src, type, ref_idx, terms, lo, hi, pitch, plane);
+  else hipLaunchKernelGGL(k_vel_terms<false>, g, dim3(256), 0, s, src, type, ref_idx, terms, lo, hi, pitch, plane);
+  return hipGetLastError();
+}
+
+int cub_grid(int64_t n, int ipt, int grid_cap) {
+  const int64_t tile = 256LL * ipt, tiles = (n + tile - 1) / tile;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, grid_cap));
+}
+
+hipError_t launch_cub_tree(const float* terms, int64_t n, int ipt, int vec, int grid_cap, float* partials,
+                           ConvState* conv, float* hist_slot, hipStream_t s) {
+  const int grid = cub_grid(n, ipt, grid_cap);
+  hipLaunchKernelGGL(k_cub_pass1, dim3(grid), dim3(256), 0, s, terms, n, ipt, vec, partials, conv);
+  hipLaunchKernelGGL(k_cub_pass2, dim3(1), dim3(256), 0, s, partials, grid, conv, hist_slot);
   return hipGetLastError();
 }
 

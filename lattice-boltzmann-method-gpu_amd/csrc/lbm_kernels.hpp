@@ -47,7 +47,9 @@ struct Layout {
 // collide, one wavefront per active 256-cell chunk (or 64-cell quarter chunk), every
 // neighbour a plain pull.  Boundary values are stored producer-side into the slots their one
 // consumer pulls next step: wall bounce-back, and the NEE value of an NEE neighbour.
-// Partials: one fp64 |u| sum per block (reduction blocks, then chunk blocks).
+// 4-cell ranges leave their NEE-adjacent fluid cells to NEE blocks that lead the grid, one
+// cell per thread; one-cell ranges do them in their quarter waves.
+// Partials: one fp64 |u| sum per block (reduction blocks, NEE blocks, then chunk blocks).
 struct MainArgs {
   const float* src;     // base (past the guard chunk)
   float* dst;
@@ -85,6 +87,14 @@ struct MainArgs {
   unsigned long long* exact_waves;  // counts 4-cell waves that fell back to the exact division
   const int* stopped;   // nullable
   float omc;            // the reference's (1.0f - 1.0f / tau)
+  // NEE-adjacent fluid cells of a 4-cell range (NEE blocks: one thread per cell)
+  const int* cells;         // linear ids, grouped by NEE-link mask
+  const uint32_t* cell_nl;  // their NEE-link masks
+  const float4* nee_bc;     // kNeeSlots records per cell: the boundary data of its first NEE
+                            // directions, gathered once (static)
+  int n_nee;
+  int nee_blocks;           // multiple of 8 (keeps the chunk blocks' XCD order)
+  int nee_waves;            // active waves per NEE block (1 for short, scattered lists)
   int swap;             // 1: storage rows run along physical y (Layout::swap)
   // The previous step's residual inside this launch (single domain, one cell per lane, no
   // convergence control): red_blocks (0 or 8) extra blocks lead the grid; the first sums
@@ -119,6 +129,17 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
+// NEE directions of a cell whose boundary data is loaded ahead (one flat face: 5); a cell
+// with more (edges and corners of several faces) loads the rest where they are used
+constexpr int kNeeSlots = 5;
+// nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of nl[i]
+hipError_t launch_nee_gather(const int* cells, const uint32_t* nl, const float* rho, const float* ux,
+                             const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
+                             int swap, hipStream_t s);
+// 1 active wave per NEE block for short, scattered lists (contiguous = fraction of list
+// neighbours that are storage neighbours: their lanes share lines), else 4
+int nee_waves_for(int n, double contiguous);
+int nee_grid(int n, int waves);
 int main_grid(int nchunks, bool quarter);
 constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
 constexpr int kReduceBlocks = 256;
@@ -129,6 +150,16 @@ hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvStat
                          int finish, hipStream_t s,
                          double* local_out = nullptr);  // where the sum goes (default conv->s_local)
 hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s);
+// Reference-order fp32 residual (lbm_set_residual_order LBM_SUM_CUB_TREE): the step's |u|
+// terms into their reference storage slots terms[ref_idx[c]] (fluid cells; the other slots
+// stay 0), then CUB's two-pass device-reduction tree over terms[0 .. n) -- pass 1: `grid`
+// blocks of 256 threads over tiles of 256 * ipt items (even share), pass 2: one block over the
+// partials, then the residual logic on S = 0.f + the tree's sum
+hipError_t launch_vel_terms(const float* src, const uint8_t* type, const int* ref_idx, float* terms, int64_t lo,
+                            int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
+int cub_grid(int64_t n, int ipt, int grid_cap);
+hipError_t launch_cub_tree(const float* terms, int64_t n, int ipt, int vec, int grid_cap, float* partials,
+                           ConvState* conv, float* hist_slot, hipStream_t s);
 // lazy macros: (rho, u) of the fluid cells in [lo, hi) from the last step's source buffer
 hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
                           int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);

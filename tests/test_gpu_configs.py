@@ -91,6 +91,56 @@ def test_default_loop_converges_like_oracle(gpu, name):
     lat.close()
 
 
+@pytest.mark.parametrize("name,params", [("ldc64_two_phase", "cub_i16_v4_g240"), ("poiseuille64", "thrust_i20_v2_g240")])
+def test_reference_order_residual_stop_step(gpu, name, params):
+    """lbm_set_residual_order(LBM_SUM_CUB_TREE): the |u| terms in the reference's storage order
+    summed in fp32 by thrust::reduce's CUB tree.  The default loop stops at exactly the oracle's
+    step under the same tree (tests/golden/residual_order.json, make_residual_order.py), with
+    the same last residual and field bits there -- 5084 / 6334, against 5080 / 6333 with the
+    default fp64 sum and 5711 / 6230 with a serial fp32 sum."""
+    import lbm_amd
+    from lbm_amd import cases
+    g = json.load(open(os.path.join(GOLDEN, "residual_order.json")))[name][params]
+    if name.startswith("ldc"):
+        lat, geo = cases.ldc(64)
+        fluid = geo == 3
+    else:
+        lat, geo = cases.poiseuille(64, 64, 64)
+        fluid = geo == 4
+    lat.set_residual_order(lbm_amd.LBM_SUM_CUB_TREE, *g["params_ipt_vec_grid"])
+    lat.set_convergence(True, 10000, 50, 1e-6)
+    lat.step(10001, history=False)
+    st = lat.state()
+    assert st["stopped"] == 1 and st["k"] == g["stop_k"], (st["k"], g["stop_k"])
+    assert np.float32(st["residual"]) == np.float32(g["residual"])
+    assert _sha_fluid(lat.macros(), fluid) == g["sha256_macros_fluid_stop"]
+    lat.close()
+
+
+@pytest.mark.parametrize("case", ["ldc_ragged", "bifurcation"])
+def test_reference_order_residual_history(gpu, case):
+    """The CUB-tree residual history step by step against the oracle's, bit for bit: the LDC
+    brick order on a box that is not a multiple of the 8-cell bricks, and index_transform's
+    compact order on the shipped bifurcation (several tiles per block: grid_cap 3)."""
+    import lbm_amd
+    import orc
+    from lbm_amd import cases
+    if case == "ldc_ragged":
+        lat, geo = cases.ldc(36, 27, 21)
+        o = orc.Oracle(orc.LDC, geo, 0.55, ldc_order=orc.TWO_PHASE)
+        params = (16, 4, 240)
+    else:
+        lat, geo, inl, outl = cases.bifurcation(1)
+        o = orc.Oracle(orc.MASK, geo, 0.55, inlet_uy=inl, outlet_uy=outl)
+        params = (20, 2, 3)
+    lat.set_residual_order(lbm_amd.LBM_SUM_CUB_TREE, *params)
+    o.residual_cub_tree(*params)
+    h = lat.step(60)
+    oh = o.step(60)
+    assert np.array_equal(np.asarray(h, np.float32).view(np.uint32), np.asarray(oh, np.float32).view(np.uint32))
+    lat.close()
+
+
 def test_drivers_default_loop_stop_step(gpu, tmp_path):
     """bin/ldc and bin/poiseuille with no size arguments (the reference's 64^3 mains, C1):
     snapshots every 500 steps, then the final snapshot named by the pinned stop step, and the

@@ -134,3 +134,70 @@ def test_generic_nee_matches_coronary_expressions(oracle):
     e_upd = oracle.feq(1.05, 0.0, 0.0, 0.0123)
     e_bc = oracle.feq_bc(1.05, 0.0, 0.0, 0.0123)
     assert np.array_equal(np.delete(e_upd, 14), np.delete(e_bc, 14))
+
+
+def _cub_reduce_py(v, ipt, vec, grid_cap):
+    """Independent restatement of CUB's two-pass device reduction (pure Python, fp32 via numpy
+    scalars): even-share tiles of 256 * ipt items, per-thread serial folds (vectorised loads of
+    full tiles, striped partial tiles), 32-lane shuffle-down warp trees, warp sums in order,
+    a second single-block pass over the partials, then 0.f + S."""
+    f32 = np.float32
+    n = len(v)
+    tile = 256 * ipt
+    tiles = -(-n // tile)
+    grid = 1 if tiles <= 1 else min(tiles, grid_cap)
+    avg, big = tiles // grid, tiles - (tiles // grid) * grid
+
+    def block(agg, num_valid):
+        s = None
+        for w in range(8):
+            valid = min(32, num_valid - 32 * w)
+            if valid <= 0:
+                break
+            lane = list(agg[32 * w:32 * w + 32])
+            off = 1
+            while off < 32:
+                new = list(lane)
+                for l in range(32):
+                    if l + off < valid:
+                        new[l] = f32(lane[l + off] + lane[l])
+                lane = new
+                off *= 2
+            s = lane[0] if s is None else f32(s + lane[0])
+        return s
+
+    parts = []
+    for b in range(grid):
+        t0 = b * (avg + 1) if b < big else big * (avg + 1) + (b - big) * avg
+        off, end = t0 * tile, min(n, (t0 + avg + (1 if b < big else 0)) * tile)
+        agg = [None] * 256
+        num_valid = 256
+        while off + tile <= end:
+            for t in range(256):
+                for i in range(ipt // vec):
+                    for k in range(vec):
+                        x = v[off + vec * t + 256 * vec * i + k]
+                        agg[t] = x if agg[t] is None else f32(agg[t] + x)
+            off += tile
+        if off < end:
+            valid = end - off
+            if agg[0] is None:
+                num_valid = min(valid, 256)
+            for t in range(256):
+                for i in range(t, valid, 256):
+                    agg[t] = v[off + i] if agg[t] is None else f32(agg[t] + v[off + i])
+        parts.append(block(agg, num_valid))
+    agg = [None] * 256
+    for t in range(256):
+        for i in range(t, grid, 256):
+            agg[t] = parts[i] if agg[t] is None else f32(agg[t] + parts[i])
+    return float(f32(f32(0.0) + block(agg, min(grid, 256))))
+
+
+@pytest.mark.parametrize("n,ipt,vec,cap", [(5000, 16, 4, 240), (70000, 20, 2, 3), (33000, 16, 4, 5), (300, 16, 4, 240)])
+def test_cub_tree_restated_twice(oracle, n, ipt, vec, cap):
+    """orc_cub_reduce (the oracle's C restatement of thrust::reduce's CUB tree, the residual
+    order liblbm's LBM_SUM_CUB_TREE must match) equals an independent Python restatement bit for
+    bit: several tiles per block, partial last tiles, a single partial tile."""
+    v = np.random.RandomState(n).rand(n).astype(np.float32) * np.float32(1e-3)
+    assert np.float32(oracle.cub_reduce(v, ipt, vec, cap)) == np.float32(_cub_reduce_py(list(v), ipt, vec, cap))
