@@ -165,15 +165,21 @@ typedef enum {
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
                                    asynchronous RCCL error always aborts promptly. */
-  LBM_TUNE_GRID_STRIDE = 6,    /* 4-cell step kernel: 0 (default) by sparsity -- 2 blocks per CU
-                                   whose waves loop over their XCD's chunks when the chunks' lanes
-                                   are under 3/4 busy, else one chunk per wave; 1 one chunk per
-                                   wave; B = 2..8 the loop with at most B blocks per CU (sparse
-                                   chunk lists only) */
+  LBM_TUNE_GRID_STRIDE = 6,    /* 4-cell step kernel: 0 (default) by sparsity -- group lists
+                                   (LBM_TUNE_GROUPS) loop with 4 blocks per CU, chunk lists with 2
+                                   when the chunks' lanes are under 3/4 busy, else one chunk per
+                                   wave; 1 one chunk (or list slice) per wave; B = 2..8 the loop
+                                   with at most B blocks per CU (sparse lists only) */
   LBM_TUNE_INJECT_RCCL_FAULT = 7, /* test hook: 1 = the next wait of an RCCL context (lbm_sync, a
                                    synchronising lbm_step, a read-out) sees a failed peer; the knob
                                    resets itself.  Exercises the abort path below. */
-  LBM_TUNE_COUNT = 8
+  LBM_TUNE_GROUPS = 8,          /* 4-cell step kernel, sparse chunk lists: 0 (default) compact lists
+                                   of the active 4-cell groups (64 per wave) when the chunks' lanes
+                                   are under 3/4 busy, 1 never, 2 on every sparse list */
+  LBM_TUNE_GROUP_SEGMENT = 9,   /* group lists: 1..64 groups per segment (default 8: one 128-B line);
+                                   a segment with an active group enters the list whole, its idle
+                                   groups load nothing */
+  LBM_TUNE_COUNT = 10
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 
@@ -283,8 +289,10 @@ int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen
 int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_t* active_chunks);
 /* How the step kernel covers the whole-domain chunks (not a reference interface: diagnostics
  * for benchmarks and tests): cells_per_lane 1 or 4, main_blocks = its chunk workgroups,
- * grid_stride 1 when those loop over their XCD's chunks (LBM_TUNE_GRID_STRIDE), lane_fill =
- * mean share of chunk lanes with a cell to update.  Nullable outputs. */
+ * grid_stride 1 when those loop over their XCD's chunks (LBM_TUNE_GRID_STRIDE), 2 when its
+ * waves take compact lists of active 4-cell groups (LBM_TUNE_GROUPS); lane_fill = mean share
+ * of chunk lanes (with groups: of a listed group's cells) with a cell to update.  Nullable
+ * outputs. */
 int lbm_get_launch_shape(lbm_ctx* ctx, int* cells_per_lane, int* main_blocks, int* grid_stride, double* lane_fill);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (each stores its NEE
  * neighbours' values, producer side). */

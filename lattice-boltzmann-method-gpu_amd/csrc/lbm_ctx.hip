@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -61,6 +61,9 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   uint32_t* cell_nl = nullptr;  // their NEE-link masks
   float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
+  int* groups = nullptr;  // 4-cell path, sparse ranges: compact list of active 4-cell groups
+  int64_t ngroups = 0;
+  double group_fill = 0.0;  // mean share of a listed group's cells the wave updates
   unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
   double* part = nullptr; // one |u| partial per block (NEE blocks, then chunk blocks)
   int npart = 0;
@@ -320,6 +323,8 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
+  a.groups = r.quarter ? nullptr : r.groups;
+  a.ngroups = r.ngroups;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
@@ -462,13 +467,60 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     }
   }
   r.main_blocks = main_grid(r.nchunks, r.quarter);
+  // Compact 4-cell groups (LBM_TUNE_GROUPS): on a sparse chunk list whose lanes are mostly idle
+  // (vessel trees), the wave's VALU work is the same whether a lane holds a cell or not, so
+  // idle lanes cost issue time.  The groups holding a cell to update go into one compact list
+  // in storage order, 64 per wave; runs of neighbouring groups keep their loads and stores
+  // contiguous, and a group whose list neighbour is not its row neighbour loads its x-edge
+  // cells itself (pull_issue).
+  {
+    const int gm = g_tune[LBM_TUNE_GROUPS];
+    const bool want = gm == 2 || (gm == 0 && r.lane_masks && r.lane_fill < 0.75);
+    if (!r.quarter && r.nchunks && r.chunk0 < 0 && want) {
+      // segments of seg groups (LBM_TUNE_GROUP_SEGMENT, default 8 = one 128-B line of a chunk
+      // slice): a segment with an active group enters the list whole, its idle groups marked
+      // (bit 0) so their lanes load nothing.  Whole lines per wave load beat full lanes on the
+      // coronary tree (59 vs 73 us per step with single groups), and cost the upsampled
+      // bifurcation, whose runs are long anyway, 3% (profiles/r03_groups_ab.log)
+      const int seg = std::max(1, g_tune[LBM_TUNE_GROUP_SEGMENT]);
+      std::vector<int> gl;
+      int64_t cells_in = 0;
+      for (int ch : chunks)
+        for (int l0 = 0; l0 < 64; l0 += seg) {
+          int nseg = 0, ng[64];
+          for (int l = l0; l < l0 + seg && l < 64; ++l) {
+            int n = 0;
+            for (int k = 0; k < 4; ++k) {
+              const int64_t cell = (int64_t)ch * kChunk + 4 * l + k;
+              const uint8_t v = t[cell];
+              n += in(cell) && (v & kClassMask) == kFluid && !(v & kNeeAdj);
+            }
+            ng[l - l0] = n;
+            nseg += n;
+          }
+          if (!nseg) continue;
+          for (int l = l0; l < l0 + seg && l < 64; ++l) gl.push_back(ch * kChunk + 4 * l + (ng[l - l0] ? 0 : 1));
+          cells_in += nseg;
+        }
+      r.ngroups = (int64_t)gl.size();
+      r.group_fill = gl.empty() ? 1.0 : (double)cells_in / (4.0 * (double)gl.size());
+      if (r.ngroups) {
+        HIPCK(c, hipMalloc(&r.groups, sizeof(int) * gl.size()));
+        HIPCK(c, hipMemcpy(r.groups, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice));
+      }
+      const int64_t waves = (r.ngroups + 63) / 64;
+      r.main_blocks = waves ? (int)std::max<int64_t>(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
+    }
+  }
   // Sparse chunk lists loop: a partly empty chunk is too little work for a wave of its own
   // (the upsampled bifurcation: +12% with two blocks per CU looping over their XCD's chunks).
   // Full chunks do not: boxes and the pipe run 10-13% slower that way (lockstep waves,
   // profiles/r02_grid_stride_ab.log), so they keep one chunk per wave.
   const int gs = g_tune[LBM_TUNE_GRID_STRIDE];
-  const int per_cu = gs >= 2 ? gs : (gs == 0 && r.lane_masks && r.lane_fill < 0.75) ? 2 : 0;
-  if (!r.quarter && r.lane_masks && per_cu > 0) {  // the loop kernel is the lane-mask one
+  // group lists loop with four blocks per CU by default (interleaved A/B: C4 x4 -3.7%, coronary
+  // tree -0.6% against one list slice per wave; profiles/r03_groups_ab.log)
+  const int per_cu = gs >= 2 ? gs : gs == 1 ? 0 : r.groups ? 4 : (r.lane_masks && r.lane_fill < 0.75) ? 2 : 0;
+  if (!r.quarter && (r.lane_masks || r.groups) && per_cu > 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->d.device) != hipSuccess || cus <= 0)
       cus = 256;
@@ -487,6 +539,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
 void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.lane_masks) (void)hipFree(r.lane_masks);
+  if (r.groups) (void)hipFree(r.groups);
   if (r.cells) (void)hipFree(r.cells);
   if (r.cell_nl) (void)hipFree(r.cell_nl);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
@@ -604,7 +657,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 1};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 1, 2, 64};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1545,8 +1598,8 @@ int lbm_get_launch_shape(lbm_ctx* c, int* cells_per_lane, int* main_blocks, int*
   if (!c) return LBM_ERR_ARG;
   if (cells_per_lane) *cells_per_lane = c->whole.quarter ? 1 : 4;
   if (main_blocks) *main_blocks = c->whole.main_blocks;
-  if (grid_stride) *grid_stride = c->whole.stride ? 1 : 0;
-  if (lane_fill) *lane_fill = c->whole.lane_fill;
+  if (grid_stride) *grid_stride = c->whole.groups ? 2 : c->whole.stride ? 1 : 0;
+  if (lane_fill) *lane_fill = c->whole.groups ? c->whole.group_fill : c->whole.lane_fill;
   return LBM_OK;
 }
 

@@ -89,14 +89,16 @@ constexpr int64_t cell_off(int pitch, int64_t plane) {
 
 // Pull of population Q for the lane's 4 cells c..c+3 from c - e_Q .. c+3 - e_Q, in two
 // phases so that all of a wave's loads are in flight together (one round trip per wave):
-//  issue:   the aligned 16-B slice at c - (e_Q with e_x = 0), and for e_x != 0 the one
-//           float the wave's edge lane needs from the neighbouring chunk (all lanes load the
-//           same address, no branch);
-//  compose: shift the slice by one cell across lanes (DPP) and drop the edge float into
-//           lane 0 (e_x = +1) or lane 63 (e_x = -1).
+//  issue:   the aligned 16-B slice at c - (e_Q with e_x = 0), and for e_x != 0 the one float
+//           beyond the lane's run of cells: cell lo - 1 (e_x = +1) or hi (e_x = -1), where
+//           [lo, hi) is the wave's chunk (all lanes load the same address, no branch) or, for a
+//           wave of compact groups (GROUPS), the lane's own 4 cells;
+//  compose: shift the slice by one cell across lanes (DPP) and take the edge float instead
+//           where the neighbouring lane does not hold the neighbouring cells (take_lo / take_hi:
+//           lane 0 / 63 of a chunk; a group whose list neighbour is not its row neighbour).
 template <int Q, bool SW>
-__device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t cb, int64_t c,
-                                           int pitch, int64_t plane, bool need) {
+__device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restrict__ src, int64_t lo, int64_t hi,
+                                           int64_t c, int pitch, int64_t plane, bool need) {
   const int64_t ro = row_off<Q, SW>(pitch, plane);
   // lanes outside the chunk's lane mask (sparse lattices) all read the buffer's first line,
   // which stays cached: no HBM bytes for them, and no branch (a branch per direction made the
@@ -112,36 +114,37 @@ __device__ __forceinline__ void pull_issue(f4& a, float& e, const float* __restr
   // load, which only the scalar cache and L2 serve (0.30 GB less HBM read per launch at 512^3,
   // +1.8-2.7% in interleaved A/B runs, profiles/r02_edge_vector_ab.log).  The empty asm moves
   // the offset to a VGPR.
-  if constexpr (SDir<Q, SW>::x == 1) {  // lane 0: b - 1
-    int64_t o = aidx(cb - ro - 1, Q);
+  if constexpr (SDir<Q, SW>::x == 1) {  // cell lo - 1
+    int64_t o = aidx(lo - ro - 1, Q);
     asm volatile("" : "+v"(o));
     e = src[o];
-  } else if constexpr (SDir<Q, SW>::x == -1) {  // lane 63: b + 4
-    int64_t o = aidx(cb + kChunk - ro, Q);
+  } else if constexpr (SDir<Q, SW>::x == -1) {  // cell hi
+    int64_t o = aidx(hi - ro, Q);
     asm volatile("" : "+v"(o));
     e = src[o];
   }
 }
 
 template <int Q, bool SW>
-__device__ __forceinline__ f4 pull_compose(const f4 a, float e, int lane) {
+__device__ __forceinline__ f4 pull_compose(const f4 a, float e, bool take_lo, bool take_hi) {
   if constexpr (SDir<Q, SW>::x == 0) {
     return a;
   } else if constexpr (SDir<Q, SW>::x == 1) {  // needs b-1 .. b+2
     const float p = lane_from_prev(a.w);
-    return f4{lane == 0 ? e : p, a.x, a.y, a.z};
+    return f4{take_lo ? e : p, a.x, a.y, a.z};
   } else {                                 // needs b+1 .. b+4
     const float n = lane_from_next(a.x);
-    return f4{a.y, a.z, a.w, lane == 63 ? e : n};
+    return f4{a.y, a.z, a.w, take_hi ? e : n};
   }
 }
 
 template <bool SW, int... Qs>
-__device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t cb, int64_t c, int lane,
-                                          int pitch, int64_t plane, bool need, std::integer_sequence<int, Qs...>) {
+__device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, int64_t lo, int64_t hi, int64_t c,
+                                          bool take_lo, bool take_hi, int pitch, int64_t plane, bool need,
+                                          std::integer_sequence<int, Qs...>) {
   float e[kQ];
-  ((pull_issue<Qs, SW>(v[Qs], e[Qs], src, cb, c, pitch, plane, need)), ...);
-  ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], lane)), ...);
+  ((pull_issue<Qs, SW>(v[Qs], e[Qs], src, lo, hi, c, pitch, plane, need)), ...);
+  ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], take_lo, take_hi)), ...);
 }
 
 template <int J, int... Qs>
@@ -339,15 +342,39 @@ __device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
 //        branch) the exact division, counted in exact_waves.  Both paths cost 216-220 VGPRs
 //        against 170 for one -- no occupancy change: either way two waves per SIMD.
-template <bool FAST, bool SW, bool MASK>
+template <bool FAST, bool SW, bool MASK, bool GROUPS = false>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
   double acc = 0.0;
-  const int64_t c = cb + lane * 4;
-  // lanes the chunk's mask leaves out hold no fluid cell and neighbour none: they load nothing
-  // and count as passive (nothing stored, no |u|)
-  const bool need = MASK ? ((lane_mask >> lane) & 1u) != 0 : true;
+  int64_t c;
+  bool need, take_lo, take_hi;
   f4 v[kQ];
-  pull4_all<SW>(v, a.src, cb, c, lane, a.pitch, a.plane, need, AllQ{});
+  if constexpr (GROUPS) {
+    // compact groups: lane = one 4-cell group of the range's list (cb: the wave's first entry);
+    // a lane takes its x-neighbours' cells from the neighbouring lane when that lane holds the
+    // neighbouring group of the row, else by its own edge loads
+    // entries: the group's first cell (a multiple of 4), bit 0 set for an idle group of a
+    // segment (it loads nothing); the tail lanes of the last wave read entry 0 and idle too
+    const int64_t gi = cb + lane;
+    const int e = a.groups[gi < a.ngroups ? gi : 0];
+    need = gi < a.ngroups && !(e & 1);
+    const int g = e & ~3;
+    // a neighbour lane that loads nothing or holds another row position is no x-neighbour
+    const int nd = need ? g : -8;
+    const int gp = __builtin_amdgcn_mov_dpp(nd, 0x138, 0xf, 0xf, false);  // lane - 1 (wave_shr:1)
+    const int gn = __builtin_amdgcn_mov_dpp(nd, 0x130, 0xf, 0xf, false);  // lane + 1 (wave_shl:1)
+    take_lo = lane == 0 || gp + 4 != g;
+    take_hi = lane == 63 || gn != g + 4;
+    c = g;
+    pull4_all<SW>(v, a.src, c, c + 4, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
+  } else {
+    c = cb + lane * 4;
+    // lanes the chunk's mask leaves out hold no fluid cell and neighbour none: they load
+    // nothing and count as passive (nothing stored, no |u|)
+    need = MASK ? ((lane_mask >> lane) & 1u) != 0 : true;
+    take_lo = lane == 0;
+    take_hi = lane == 63;
+    pull4_all<SW>(v, a.src, cb, cb + kChunk, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
+  }
   const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
   const unsigned t4 = need ? t4r : 0u;
   // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
@@ -580,7 +607,7 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
   return a.chunk0 >= 0 ? (int64_t)a.chunk0 + idx : (int64_t)a.chunks[idx];
 }
 
-template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false>
+template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false, bool GROUPS = false>
 __device__ __forceinline__ void step_body(const MainArgs& a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -608,7 +635,16 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
-    if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
+    if constexpr (GROUPS && STRIDE) {  // compact groups, grid-stride over XCD (b & 7)'s eighth of the list
+      const int64_t nw = (a.ngroups + 63) >> 6;  // 64-entry wave loads
+      const int64_t per = (nw + 7) >> 3;
+      const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
+      const int step = (a.main_blocks >> 3) * (kBlock / 64);
+      for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step)
+        acc += process_chunk<FAST, SW, false, true>(a, i * 64, lane, 0);
+    } else if constexpr (GROUPS) {  // compact 4-cell groups: wave idx takes list entries 64 idx ..
+      if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true>(a, (int64_t)idx * 64, lane, 0);
+    } else if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
         acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
     } else if constexpr (STRIDE) {  // grid-stride: XCD (b & 7) takes its eighth of the list in order
@@ -638,9 +674,9 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
 
 // 4 cells per lane (big lattices): two waves per SIMD (216-220 VGPRs); MASK: the range has
 // lane masks (sparse chunk lists)
-template <bool FAST, bool SW, bool MASK, bool STRIDE = false>
+template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
-  step_body<FAST, false, SW, MASK, STRIDE>(a);
+  step_body<FAST, false, SW, MASK, STRIDE, GROUPS>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
 template <bool SW>
@@ -1242,6 +1278,14 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   const size_t lds = 0;
   if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
     k = sw ? k_step1<true> : k_step1<false>;
+  } else if (a.groups) {
+    if (a.chunk_stride) {
+      if (a.fast_div) k = sw ? k_step<true, true, false, true, true> : k_step<true, false, false, true, true>;
+      else k = sw ? k_step<false, true, false, true, true> : k_step<false, false, false, true, true>;
+    } else {
+      if (a.fast_div) k = sw ? k_step<true, true, false, false, true> : k_step<true, false, false, false, true>;
+      else k = sw ? k_step<false, true, false, false, true> : k_step<false, false, false, false, true>;
+    }
   } else if (a.fast_div) {
     if (a.chunk_stride) k = sw ? k_step<true, true, true, true> : k_step<true, false, true, true>;
     else if (a.lane_masks) k = sw ? k_step<true, true, true> : k_step<true, false, true>;

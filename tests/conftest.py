@@ -51,12 +51,15 @@ def knob(lbm):
         lbm.tune(which, prev)
 
 
-@pytest.fixture(params=["4", "1"], ids=["4cells", "1cell"])
+@pytest.fixture(params=["4", "4g", "1"], ids=["4cells", "4groups", "1cell"])
 def cells_per_lane(request, knob, lbm):
-    """Run a parity test through both stream-collide paths: four cells per lane (the
-    bandwidth path) and one cell per lane (what small lattices use by default)."""
-    knob(lbm.TUNE_CELLS_PER_LANE, int(request.param))
-    return int(request.param)
+    """Run a parity test through every stream-collide path: four cells per lane over whole
+    chunks (the bandwidth path), four cells per lane over compact lists of active 4-cell groups
+    (sparse lattices; forced on every sparse chunk list), and one cell per lane (what small
+    lattices use by default)."""
+    knob(lbm.TUNE_CELLS_PER_LANE, 4 if request.param.startswith("4") else 1)
+    knob(lbm.TUNE_GROUPS, 2 if request.param == "4g" else 1)
+    return 4 if request.param.startswith("4") else 1
 
 
 @pytest.fixture(params=["x", "y"], ids=["xrows", "yrows"])

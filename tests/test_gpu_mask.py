@@ -127,8 +127,8 @@ def test_bifurcation_upsampled_bitwise(gpu, oracle):
     oracle's geo_pre, and the lattice steps bit for bit like the oracle."""
     from lbm_amd import cases, index_transform
     lat, up = cases.bifurcation_upsampled(4)
-    shape = lat.launch_shape()  # a sparse list: the chunk waves loop (LBM_TUNE_GRID_STRIDE auto)
-    assert shape["cells_per_lane"] == 4 and shape["grid_stride"] == 1 and shape["lane_fill"] < 0.75, shape
+    shape = lat.launch_shape()  # half-empty chunks: compact lists of 4-cell groups (LBM_TUNE_GROUPS auto)
+    assert shape["cells_per_lane"] == 4 and shape["grid_stride"] == 2, shape
     geo = oracle.geo_mask(up.astype(np.int32))
     got = lat.geo()
     assert np.array_equal(got, geo), f"{np.count_nonzero(got != geo)} codes differ"
@@ -159,6 +159,7 @@ def test_grid_stride_bitwise(gpu, knob, case):
     above and by test_gpu_parity.py."""
     from lbm_amd import cases
     knob(gpu.TUNE_CELLS_PER_LANE, 4)
+    knob(gpu.TUNE_GROUPS, 1)  # chunk waves (the group lists have their own test below)
     knob(gpu.TUNE_ROW_AXIS, 2)  # rows along the pipe: one chunk per (x, z) column, lanes full
 
     def run(v):
@@ -179,3 +180,39 @@ def test_grid_stride_bitwise(gpu, knob, case):
         # the residual's fp64 |u| sum is accumulated per block, so the launch shape may move its
         # last bits: the fp32 sums S_k agree to an ulp, the residuals to ~1e-7 absolute (lbm.h)
         assert np.all(np.isfinite(h)) and np.allclose(h, h0, rtol=0, atol=2e-7), (v, h, h0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["bif_x4", "coronary", "pipe"])
+def test_groups_bitwise(gpu, knob, case):
+    """LBM_TUNE_GROUPS changes only which lane updates which cells: the upsampled bifurcation and
+    the coronary tree (compact 4-cell group lists by default) with the lists off, and a pipe
+    (whole chunks by default) with them forced on, step bit for bit like their defaults --
+    which the oracle pins (test_bifurcation_upsampled_bitwise, tests with the cells_per_lane
+    fixture's "4groups" path)."""
+    from lbm_amd import cases
+    knob(gpu.TUNE_CELLS_PER_LANE, 4)
+
+    def build():
+        if case == "bif_x4":
+            return cases.bifurcation_upsampled(4)[0]
+        if case == "coronary":
+            return cases.coronary(cases.coronary_reference_vessel())[0]
+        return cases.poiseuille(64, 256, 64)[0]
+
+    def run(v):
+        with gpu.tuned(gpu.TUNE_GROUPS, v):
+            lat = build()
+        shape = lat.launch_shape()
+        hist = lat.step(12)
+        f = lat.f()
+        lat.close()
+        return shape, f, hist
+
+    s0, f0, h0 = run(0)
+    assert s0["grid_stride"] == (0 if case == "pipe" else 2), s0
+    s1, f1, h1 = run(2 if case == "pipe" else 1)
+    assert s1["grid_stride"] == (2 if case == "pipe" else 1), s1
+    assert np.array_equal(f1.view(np.uint32), f0.view(np.uint32)), case
+    # per-block fp64 partials: the launch shape may move the residual's last bits (lbm.h)
+    assert np.all(np.isfinite(h1)) and np.allclose(h1, h0, rtol=0, atol=2e-7), (h1, h0)
