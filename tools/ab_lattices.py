@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B of liblbm builds on the bench's secondary lattices (run through gpurun).
 
-    python3 tools/ab_lattices.py <rounds> <variant> ...     # variant: product | a dir with liblbm.so
+    python3 tools/ab_lattices.py <rounds> <variant> ...     # variant: product | a dir with liblbm.so,
+                                                            # optionally "@knob:value,..." (lbm_tune)
     python3 tools/ab_lattices.py --child <cases>            # one process per (round, variant)
 
 Each (round, variant) is a fresh process with LBM_LIBRARY pointing at the variant, so builds
@@ -23,8 +24,13 @@ def child(which):
     import torch  # noqa: F401
     import lbm_amd
     from lbm_amd import cases
+    for kv in filter(None, os.environ.get("AB_TUNE", "").split(",")):  # "knob:value,...": lbm_tune
+        k, v = kv.split(":")
+        lbm_amd.tune(int(k), int(v))
 
     def run(lat, steps):
+        shape = lat.launch_shape()
+        nf = lat.counts()["n_fluid"]
         lat.step(20, history=False)
         lat.sync()
         t = time.perf_counter()
@@ -36,7 +42,8 @@ def child(which):
         st = lat.stats()
         lat.close()
         return {"us_step": round(dt / steps * 1e6, 2),
-                "k_step_us": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]) * 1e3, 2)}
+                "k_step_us": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]) * 1e3, 2),
+                "n_fluid": nf, "launch_shape": shape}
 
     out = {}
     for w in which.split(","):
@@ -62,10 +69,12 @@ def main():
     for r in range(rounds):
         for v in variants:
             env = dict(os.environ)
-            if v == "product":
+            lib, _, tune = v.partition("@")
+            env["AB_TUNE"] = tune
+            if lib == "product":
                 env.pop("LBM_LIBRARY", None)
             else:
-                env["LBM_LIBRARY"] = os.path.join(REPO, v, "liblbm.so")
+                env["LBM_LIBRARY"] = os.path.join(REPO, lib, "liblbm.so")
             p = subprocess.run([sys.executable, __file__, "--child", which], env=env, capture_output=True, text=True,
                                timeout=600)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("AB ")]
