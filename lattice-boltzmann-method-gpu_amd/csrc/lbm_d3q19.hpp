@@ -82,67 +82,99 @@ LBM_HD uint8_t make_nee(int face, bool pressure) {
 
 // f^eq_q in the form of the update kernels (ldc.cu:330-348, Poiseulle.cu:543-561,
 // bifurcation.cu:587-624), one q at a time.  Expression trees and literal types are the
-// reference's, including the fp64 "3.0*tmp_uz*tmp_uz" of q = 14 (ldc.cu:344).
+// reference's, including the fp64 "3.0*tmp_uz*tmp_uz" of q = 14 (ldc.cu:344).  Each is
+// (tmp_rho / w_q) * P_q(u) with the quotient rounded first, as C evaluates the reference's
+// "tmp_rho /36.0f * (...)"; feq_pre<Q> takes that quotient precomputed (the step kernels
+// form it with an exact shortcut, see kernels), feq<Q> divides here.
+template <int Q> struct FeqW;   // w_q's divisor: 3, 18 or 36
 template <int Q>
-LBM_HD float feq(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz);
-
-template <> LBM_HD float feq<0>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho/3.0f * (1.0f - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy -1.5f* tmp_uz*tmp_uz);
+LBM_HD auto feq_poly(float tmp_ux, float tmp_uy, float tmp_uz);
+template <> struct FeqW<0> { static constexpr float d = 3.0f; };
+template <> struct FeqW<1> { static constexpr float d = 18.0f; };
+template <> struct FeqW<2> { static constexpr float d = 18.0f; };
+template <> struct FeqW<3> { static constexpr float d = 18.0f; };
+template <> struct FeqW<4> { static constexpr float d = 18.0f; };
+template <> struct FeqW<5> { static constexpr float d = 18.0f; };
+template <> struct FeqW<6> { static constexpr float d = 18.0f; };
+template <> struct FeqW<7> { static constexpr float d = 36.0f; };
+template <> struct FeqW<8> { static constexpr float d = 36.0f; };
+template <> struct FeqW<9> { static constexpr float d = 36.0f; };
+template <> struct FeqW<10> { static constexpr float d = 36.0f; };
+template <> struct FeqW<11> { static constexpr float d = 36.0f; };
+template <> struct FeqW<12> { static constexpr float d = 36.0f; };
+template <> struct FeqW<13> { static constexpr float d = 36.0f; };
+template <> struct FeqW<14> { static constexpr float d = 36.0f; };
+template <> struct FeqW<15> { static constexpr float d = 36.0f; };
+template <> struct FeqW<16> { static constexpr float d = 36.0f; };
+template <> struct FeqW<17> { static constexpr float d = 36.0f; };
+template <> struct FeqW<18> { static constexpr float d = 36.0f; };
+template <> LBM_HD auto feq_poly<0>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy -1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<1>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /18.0f * (1.0f + 3.0f* tmp_ux + 3.0f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy -1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<1>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* tmp_ux + 3.0f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy -1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<2>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /18.0f * (1.0f - 3.0f* tmp_ux + 3.0f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy -1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<2>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 3.0f* tmp_ux + 3.0f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy -1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<3>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /18.0f * (1.0f + 3.0f* tmp_uy + 3.0f*tmp_uy*tmp_uy - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<3>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* tmp_uy + 3.0f*tmp_uy*tmp_uy - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<4>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /18.0f * (1.0f - 3.0f* tmp_uy + 3.0f*tmp_uy*tmp_uy - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<4>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 3.0f* tmp_uy + 3.0f*tmp_uy*tmp_uy - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<5>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /18.0f * (1.0f + 3.0f* tmp_uz + 3.0f*tmp_uz*tmp_uz - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy);
+template <> LBM_HD auto feq_poly<5>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* tmp_uz + 3.0f*tmp_uz*tmp_uz - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy);
 }
-template <> LBM_HD float feq<6>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /18.0f* (1.0f - 3.0f* tmp_uz + 3.0f*tmp_uz*tmp_uz - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy);
+template <> LBM_HD auto feq_poly<6>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 3.0f* tmp_uz + 3.0f*tmp_uz*tmp_uz - 1.5f*tmp_ux*tmp_ux -1.5f* tmp_uy*tmp_uy);
 }
-template <> LBM_HD float feq<7>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f* (1.0f + 3.0f* (tmp_ux + tmp_uy) + 3.0f*tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy + 9.0f*tmp_ux*tmp_uy -1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<7>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_ux + tmp_uy) + 3.0f*tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy + 9.0f*tmp_ux*tmp_uy -1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<8>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_ux - tmp_uy) + 3.0f*tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy - 9.0f*tmp_ux*tmp_uy-1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<8>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_ux - tmp_uy) + 3.0f*tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy - 9.0f*tmp_ux*tmp_uy-1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<9>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_uy - tmp_ux) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy - 9.0f*tmp_ux*tmp_uy-1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<9>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_uy - tmp_ux) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy - 9.0f*tmp_ux*tmp_uy-1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<10>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_ux + tmp_uy) + 3.0f*tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy + 9.0f*tmp_ux*tmp_uy-1.5f* tmp_uz*tmp_uz);
+template <> LBM_HD auto feq_poly<10>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 3.0f* (tmp_ux + tmp_uy) + 3.0f*tmp_ux*tmp_ux + 3.0f*tmp_uy*tmp_uy + 9.0f*tmp_ux*tmp_uy-1.5f* tmp_uz*tmp_uz);
 }
-template <> LBM_HD float feq<11>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz-1.5f* tmp_uy*tmp_uy);
+template <> LBM_HD auto feq_poly<11>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz-1.5f* tmp_uy*tmp_uy);
 }
-template <> LBM_HD float feq<12>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f* (1.0f + 3.0f* (tmp_ux - tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_ux*tmp_uz-1.5f* tmp_uy*tmp_uy);
+template <> LBM_HD auto feq_poly<12>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_ux - tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_ux*tmp_uz-1.5f* tmp_uy*tmp_uy);
 }
-template <> LBM_HD float feq<13>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_uz - tmp_ux) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_ux*tmp_uz-1.5f* tmp_uy*tmp_uy);
+template <> LBM_HD auto feq_poly<13>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_uz - tmp_ux) + 3.0f* tmp_ux*tmp_ux + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_ux*tmp_uz-1.5f* tmp_uy*tmp_uy);
 }
-template <> LBM_HD float feq<14>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  // the only fp64 sub-expression of the reference: "3.0*tmp_uz*tmp_uz" promotes the tail
-  return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz -1.5f* tmp_uy*tmp_uy);
+// the only fp64 sub-expression of the reference: "3.0*tmp_uz*tmp_uz" promotes the tail
+template <> LBM_HD auto feq_poly<14>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 3.0f* (tmp_ux + tmp_uz) + 3.0f* tmp_ux*tmp_ux + 3.0*tmp_uz*tmp_uz + 9.0f*tmp_ux*tmp_uz -1.5f* tmp_uy*tmp_uy);
 }
-template <> LBM_HD float feq<15>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_uy + tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_uy*tmp_uz- 1.5f*tmp_ux*tmp_ux);
+template <> LBM_HD auto feq_poly<15>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_uy + tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_uy*tmp_uz- 1.5f*tmp_ux*tmp_ux);
 }
-template <> LBM_HD float feq<16>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_uz - tmp_uy) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
+template <> LBM_HD auto feq_poly<16>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_uz - tmp_uy) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
 }
-template <> LBM_HD float feq<17>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f + 3.0f* (tmp_uy - tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
+template <> LBM_HD auto feq_poly<17>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f + 3.0f* (tmp_uy - tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz - 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
 }
-template <> LBM_HD float feq<18>(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
-  return tmp_rho /36.0f * (1.0f - 3.0f* (tmp_uy + tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
+template <> LBM_HD auto feq_poly<18>(float tmp_ux, float tmp_uy, float tmp_uz) {
+  return (1.0f - 3.0f* (tmp_uy + tmp_uz) + 3.0f* tmp_uy*tmp_uy + 3.0f*tmp_uz*tmp_uz + 9.0f*tmp_uy*tmp_uz - 1.5f*tmp_ux*tmp_ux);
+}
+// pre = RN(tmp_rho / w_q); the product is formed in the poly's type (double for q = 14) and
+// rounded to float once, as the reference's expression is
+template <int Q>
+LBM_HD float feq_pre(float pre, float tmp_ux, float tmp_uy, float tmp_uz) {
+  return pre * feq_poly<Q>(tmp_ux, tmp_uy, tmp_uz);
+}
+template <int Q>
+LBM_HD float feq(float tmp_rho, float tmp_ux, float tmp_uy, float tmp_uz) {
+  return feq_pre<Q>(tmp_rho / FeqW<Q>::d, tmp_ux, tmp_uy, tmp_uz);
 }
 
 // Boundary-value equilibrium of the NEE boundaries.  The reference writes these as

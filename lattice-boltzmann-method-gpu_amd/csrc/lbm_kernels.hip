@@ -205,7 +205,23 @@ __device__ __forceinline__ void moments(const f4* v, float& rho, float& ux, floa
 // (3 VALU), which equals RN(x / tau) for every x whose residual r does not underflow
 // (Markstein's theorem; the kernel's caller verifies it for the run's tau over a whole
 // binade, which covers [2^-100, 2^100] by exact power-of-two scaling).  Where |x| < 2^-100,
-// f - q == f for both quotients whenever |f| >= 2^-60, which the wave checks first.
+// f - q == f for both quotients whenever |f| >= 2^-60, which the wave checks first.  The
+// equilibria's prefactors rho/3, rho/18 and rho/36 take the same shortcut (the divisors are
+// verified by verify_fast_div too, and the wave checks 2^-60 <= |rho| < 2^45).
+__device__ __forceinline__ float fast_quot(float x, float d, float y) {
+  const float q0 = x * y;
+  return __builtin_fmaf(__builtin_fmaf(-q0, d, x), y, q0);
+}
+struct Pref {  // RN(rho / 3), RN(rho / 18), RN(rho / 36)
+  float p3, p18, p36;
+  __device__ __forceinline__ explicit Pref(float r)
+      : p3(fast_quot(r, 3.0f, 1.0f / 3.0f)), p18(fast_quot(r, 18.0f, 1.0f / 18.0f)),
+        p36(fast_quot(r, 36.0f, 1.0f / 36.0f)) {}
+  template <int Q>
+  __device__ __forceinline__ float of() const {
+    return FeqW<Q>::d == 3.0f ? p3 : FeqW<Q>::d == 18.0f ? p18 : p36;
+  }
+};
 template <int J, bool FAST, int... Qs>
 __device__ __forceinline__ void relax_cell(f4* v, float tau, float rcp, float r, float ux, float uy, float uz,
                                            std::integer_sequence<int, Qs...>) {
@@ -214,16 +230,18 @@ __device__ __forceinline__ void relax_cell(f4* v, float tau, float rcp, float r,
       const float q0 = x * rcp;
       return __builtin_fmaf(__builtin_fmaf(-q0, tau, x), rcp, q0);
     };
-    ((v[Qs][J] = v[Qs][J] - div_tau(v[Qs][J] - feq<Qs>(r, ux, uy, uz))), ...);
+    const Pref p(r);
+    ((v[Qs][J] = v[Qs][J] - div_tau(v[Qs][J] - feq_pre<Qs>(p.template of<Qs>(), ux, uy, uz))), ...);
   } else {
     ((v[Qs][J] = v[Qs][J] - (v[Qs][J] - feq<Qs>(r, ux, uy, uz)) / tau), ...);
   }
 }
 
 // the fast quotient's domain for one cell: 2^-60 <= |f_q| < 2^40 and |u| < 2^10 bound
-// |f - feq| below 2^72 (no overflow) and make quotients of |x| < 2^-100 irrelevant
+// |f - feq| below 2^72 (no overflow) and make quotients of |x| < 2^-100 irrelevant;
+// 2^-60 <= |rho| < 2^45 keeps the prefactor quotients' residuals normal
 template <int J>
-__device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, float uz) {
+__device__ __forceinline__ bool fast_div_ok(const f4* v, float r, float ux, float uy, float uz) {
   float mn = __builtin_fabsf(v[0][J]), mx = mn;
 #pragma unroll
   for (int q = 1; q < kQ; ++q) {
@@ -231,7 +249,8 @@ __device__ __forceinline__ bool fast_div_ok(const f4* v, float ux, float uy, flo
     mx = __builtin_fmaxf(mx, __builtin_fabsf(v[q][J]));
   }
   const float um = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ux), __builtin_fabsf(uy)), __builtin_fabsf(uz));
-  return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f;  // false for NaN
+  const float ar = __builtin_fabsf(r);
+  return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f && ar >= 0x1p-60f && ar < 0x1p45f;  // false for NaN
 }
 
 // ---- NEE boundaries, producer side -------------------------------------------------------
@@ -395,10 +414,10 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   bool fast_wave = false;
   if constexpr (FAST) {  // non-fluid cells are never stored: they do not constrain the wave
     const unsigned fl = t4 & (t4 >> 1) & 0x01010101u;
-    const bool ok = (!(fl & 0x1u) || fast_div_ok<0>(v, x0, y0, z0)) &&
-                    (!(fl & 0x100u) || fast_div_ok<1>(v, x1, y1, z1)) &&
-                    (!(fl & 0x10000u) || fast_div_ok<2>(v, x2, y2, z2)) &&
-                    (!(fl & 0x1000000u) || fast_div_ok<3>(v, x3, y3, z3));
+    const bool ok = (!(fl & 0x1u) || fast_div_ok<0>(v, r0, x0, y0, z0)) &&
+                    (!(fl & 0x100u) || fast_div_ok<1>(v, r1, x1, y1, z1)) &&
+                    (!(fl & 0x10000u) || fast_div_ok<2>(v, r2, x2, y2, z2)) &&
+                    (!(fl & 0x1000000u) || fast_div_ok<3>(v, r3, x3, y3, z3));
     fast_wave = __all(ok);
     if (!fast_wave && lane == 0) atomicAdd(a.exact_waves, 1ull);
   }
@@ -477,10 +496,11 @@ __device__ __forceinline__ void fix_relax_fast_all(float* f, float tau, float rc
     const float q0 = x * rcp;
     return __builtin_fmaf(__builtin_fmaf(-q0, tau, x), rcp, q0);
   };
-  ((f[Qs] = f[Qs] - div_tau(f[Qs] - feq<Qs>(r, ux, uy, uz))), ...);
+  const Pref p(r);
+  ((f[Qs] = f[Qs] - div_tau(f[Qs] - feq_pre<Qs>(p.template of<Qs>(), ux, uy, uz))), ...);
 }
 // fast_div_ok for one cell in registers
-__device__ __forceinline__ bool fast_div_ok1(const float* f, float ux, float uy, float uz) {
+__device__ __forceinline__ bool fast_div_ok1(const float* f, float r, float ux, float uy, float uz) {
   float mn = __builtin_fabsf(f[0]), mx = mn;
 #pragma unroll
   for (int q = 1; q < kQ; ++q) {
@@ -488,12 +508,13 @@ __device__ __forceinline__ bool fast_div_ok1(const float* f, float ux, float uy,
     mx = __builtin_fmaxf(mx, __builtin_fabsf(f[q]));
   }
   const float um = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ux), __builtin_fabsf(uy)), __builtin_fabsf(uz));
-  return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f;  // false for NaN
+  const float ar = __builtin_fabsf(r);
+  return mn >= 0x1p-60f && mx < 0x1p40f && um < 0x1p10f && ar >= 0x1p-60f && ar < 0x1p45f;  // false for NaN
 }
 // one cell's relaxation: the fast quotient when tau is verified and every active lane of
 // the wave lies in its domain (a wave-uniform choice: the lanes stay together), else exact
 __device__ __forceinline__ void relax1(float* f, const MainArgs& a, float r, float ux, float uy, float uz) {
-  const bool ok = fast_div_ok1(f, ux, uy, uz);
+  const bool ok = fast_div_ok1(f, r, ux, uy, uz);
   if (a.tau_fast && __all(ok)) fix_relax_fast_all(f, a.tau, a.tau_rcp, r, ux, uy, uz, AllQ{});
   else fix_relax_all(f, a.tau, r, ux, uy, uz, AllQ{});
 }
@@ -1245,6 +1266,12 @@ int grid_for(int64_t n, int block) {
 
 bool verify_fast_div(float tau) {
   if (!(tau >= 0.0625f && tau <= 16.0f)) return false;
+  // the equilibria's prefactor divisors take the same shortcut (Pref): checked once
+  static const bool consts = verify_fast_div_by(3.0f) && verify_fast_div_by(18.0f) && verify_fast_div_by(36.0f);
+  return consts && verify_fast_div_by(tau);
+}
+
+bool verify_fast_div_by(float tau) {
   const float y = 1.0f / tau;
   for (uint32_t m = 0; m < (1u << 23); ++m) {
     uint32_t bits = 0x3f800000u | m;

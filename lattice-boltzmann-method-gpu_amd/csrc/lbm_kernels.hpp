@@ -116,6 +116,7 @@ struct MainArgs {
 // power-of-two scaling, for every |x| in [2^-100, 2^100].  Exhaustive over the binade
 // (8.4 M values, a few ms on the host).
 bool verify_fast_div(float tau);
+bool verify_fast_div_by(float d);  // the same identity for any divisor d (no range check)
 
 struct ConvState {      // device-resident reference main-loop state (ldc.cu:613-685)
   double s_local;       // this rank's sum of |u| for the last step
