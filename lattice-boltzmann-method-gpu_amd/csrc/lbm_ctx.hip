@@ -323,7 +323,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
-  a.groups = r.quarter ? nullptr : r.groups;
+  a.groups = r.groups;
   a.ngroups = r.ngroups;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
@@ -442,26 +442,34 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // on a vessel tree most chunks are partly empty (the upsampled bifurcation keeps 51% of its
   // active chunks' cells).  Only for sparse chunk lists, whose waves load their chunk id
   // anyway (the mask load goes out beside it); a contiguous list would pay a round trip.
-  if (!r.quarter && r.nchunks && r.chunk0 < 0) {
+  // One-cell ranges have no masks (their idle lanes load nothing new: a wave's cells share
+  // lines); their fill -- cells to update over the active chunks' cells -- picks the group list.
+  auto updated = [&](int64_t cell) {
+    const uint8_t v = t[cell];
+    return in(cell) && (v & kClassMask) == kFluid && (r.quarter || !(v & kNeeAdj));
+  };
+  if (r.nchunks && r.chunk0 < 0) {
     std::vector<unsigned long long> lm(chunks.size());
     bool partial = false;
-    int64_t busy = 0;
+    int64_t busy = 0, cells_busy = 0;
     for (size_t j = 0; j < chunks.size(); ++j) {
       unsigned long long m = 0;
       const int64_t base = (int64_t)chunks[j] * kChunk;
       for (int l = 0; l < 64; ++l)
-        for (int k = 0; k < 4; ++k) {
-          const int64_t cell = base + 4 * l + k;
-          const uint8_t v = t[cell];
-          if (in(cell) && (v & kClassMask) == kFluid && !(v & kNeeAdj)) m |= 1ull << l;
-        }
+        for (int k = 0; k < 4; ++k)
+          if (updated(base + 4 * l + k)) {
+            m |= 1ull << l;
+            ++cells_busy;
+          }
       busy += __builtin_popcountll(m);
       m |= (m << 1) | (m >> 1);
       lm[j] = m;
       partial |= m != ~0ull;
     }
-    r.lane_fill = chunks.empty() ? 1.0 : (double)busy / (64.0 * (double)chunks.size());
-    if (partial || g_tune[LBM_TUNE_GRID_STRIDE] >= 2) {  // the loop kernel reads them
+    r.lane_fill = chunks.empty() ? 1.0
+                  : r.quarter    ? (double)cells_busy / ((double)kChunk * (double)chunks.size())
+                                 : (double)busy / (64.0 * (double)chunks.size());
+    if (!r.quarter && (partial || g_tune[LBM_TUNE_GRID_STRIDE] >= 2)) {  // the loop kernel reads them
       HIPCK(c, hipMalloc(&r.lane_masks, sizeof(unsigned long long) * lm.size()));
       HIPCK(c, hipMemcpy(r.lane_masks, lm.data(), sizeof(unsigned long long) * lm.size(), hipMemcpyHostToDevice));
     }
@@ -475,8 +483,9 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // cells itself (pull_issue).
   {
     const int gm = g_tune[LBM_TUNE_GROUPS];
-    const bool want = gm == 2 || (gm == 0 && r.lane_masks && r.lane_fill < 0.75);
-    if (!r.quarter && r.nchunks && r.chunk0 < 0 && want) {
+    const bool sparse = r.quarter ? r.lane_fill < kGroupFill1 : r.lane_masks && r.lane_fill < 0.75;
+    const bool want = gm == 2 || (gm == 0 && sparse);
+    if (r.nchunks && r.chunk0 < 0 && want) {
       // segments of seg groups (LBM_TUNE_GROUP_SEGMENT, default 8 = one 128-B line of a chunk
       // slice): a segment with an active group enters the list whole, its idle groups marked
       // (bit 0) so their lanes load nothing.  Whole lines per wave load beat full lanes on the
@@ -490,11 +499,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
           int nseg = 0, ng[64];
           for (int l = l0; l < l0 + seg && l < 64; ++l) {
             int n = 0;
-            for (int k = 0; k < 4; ++k) {
-              const int64_t cell = (int64_t)ch * kChunk + 4 * l + k;
-              const uint8_t v = t[cell];
-              n += in(cell) && (v & kClassMask) == kFluid && !(v & kNeeAdj);
-            }
+            for (int k = 0; k < 4; ++k) n += updated((int64_t)ch * kChunk + 4 * l + k);
             ng[l - l0] = n;
             nseg += n;
           }
@@ -508,7 +513,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         HIPCK(c, hipMalloc(&r.groups, sizeof(int) * gl.size()));
         HIPCK(c, hipMemcpy(r.groups, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice));
       }
-      const int64_t waves = (r.ngroups + 63) / 64;
+      const int64_t waves = (r.ngroups + (r.quarter ? 15 : 63)) / (r.quarter ? 16 : 64);
       r.main_blocks = waves ? (int)std::max<int64_t>(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
     }
   }
@@ -520,7 +525,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // group lists loop with four blocks per CU by default (interleaved A/B: C4 x4 -3.7%, coronary
   // tree -0.6% against one list slice per wave; profiles/r03_groups_ab.log)
   const int per_cu = gs >= 2 ? gs : gs == 1 ? 0 : r.groups ? 4 : (r.lane_masks && r.lane_fill < 0.75) ? 2 : 0;
-  if (!r.quarter && (r.lane_masks || r.groups) && per_cu > 0) {
+  if ((r.quarter ? r.groups && gs >= 2 : (r.lane_masks || r.groups)) && per_cu > 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->d.device) != hipSuccess || cus <= 0)
       cus = 256;

@@ -549,16 +549,10 @@ __device__ __forceinline__ void pull1w_all(float* f, const float* __restrict__ s
   ((f[Qs] = __builtin_nontemporal_load(base + rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs))), ...);
 }
 
+// one cell's collision and stores once its pulls, type byte and link masks are in
 template <bool SW>
-__device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, int l) {
-  // the pulls go out with the type byte (one round trip; the guard chunks keep every
-  // address of a lane that turns out to be idle inside the buffer)
-  const int64_t c = ch * kChunk + l;
-  const uint8_t t = a.type[c];
-  const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
-  const uint32_t nl = a.nlinks[c];
-  float f[kQ];
-  pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
+__device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, uint8_t t, uint32_t links, uint32_t nl,
+                                                float* f) {
   const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid;
   if (!in) return 0.0;
   // NEE-adjacent: the boundary data goes out now and arrives under the arithmetic below
@@ -575,6 +569,37 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, i
   if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, AllQ{});
   fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
+}
+
+template <bool SW>
+__device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, int l) {
+  // the pulls go out with the type byte (one round trip; the guard chunks keep every
+  // address of a lane that turns out to be idle inside the buffer)
+  const int64_t c = ch * kChunk + l;
+  const uint8_t t = a.type[c];
+  const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
+  const uint32_t nl = a.nlinks[c];
+  float f[kQ];
+  pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
+  return collide_cell1<SW>(a, c, t, links, nl, f);
+}
+
+// One cell per lane over a compact group list (sparse one-cell ranges): wave w takes the 16
+// entries 16 w .., lanes 4k .. 4k+3 the four cells of entry 16 w + k.  Idle entries (bit 0)
+// and the last wave's tail lanes point at a listed group, so their loads stay inside lines the
+// wave reads anyway; they store nothing.
+template <bool SW>
+__device__ __forceinline__ double process_group_cell1(const MainArgs& a, int64_t w, int lane) {
+  const int64_t gi = w * 16 + (lane >> 2);
+  const int e = a.groups[gi < a.ngroups ? gi : w * 16];
+  const bool need = gi < a.ngroups && !(e & 1);
+  const int64_t c = (int64_t)(e & ~3) + (lane & 3);
+  const uint8_t t = a.type[c];
+  const uint32_t links = a.links[c];
+  const uint32_t nl = a.nlinks[c];
+  float f[kQ];
+  pull1w_all<SW>(f, a.src, c >> 8, (int)(c & (kChunk - 1)), a.pitch, a.plane, AllQ{});  // per-lane chunk base
+  return collide_cell1<SW>(a, c, need ? t : (uint8_t)0, links, nl, f);
 }
 
 // One NEE-adjacent fluid cell of a 4-cell range (NEE blocks, one per thread; the chunk waves
@@ -656,7 +681,15 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
-    if constexpr (GROUPS && STRIDE) {  // compact groups, grid-stride over XCD (b & 7)'s eighth of the list
+    if constexpr (QUARTER && GROUPS && STRIDE) {  // the same, grid-stride over XCD (b & 7)'s eighth
+      const int64_t nw = (a.ngroups + 15) >> 4;
+      const int64_t per = (nw + 7) >> 3;
+      const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
+      const int step = (a.main_blocks >> 3) * (kBlock / 64);
+      for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step) acc += process_group_cell1<SW>(a, i, lane);
+    } else if constexpr (QUARTER && GROUPS) {  // one cell per lane over the compact group list
+      if ((int64_t)idx * 16 < a.ngroups) acc = process_group_cell1<SW>(a, idx, lane);
+    } else if constexpr (GROUPS && STRIDE) {  // compact groups, grid-stride over XCD (b & 7)'s eighth of the list
       const int64_t nw = (a.ngroups + 63) >> 6;  // 64-entry wave loads
       const int64_t per = (nw + 7) >> 3;
       const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
@@ -700,9 +733,9 @@ __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
   step_body<FAST, false, SW, MASK, STRIDE, GROUPS>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
-template <bool SW>
+template <bool SW, bool GROUPS = false, bool STRIDE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_step1(const MainArgs a) {
-  step_body<false, true, SW>(a);
+  step_body<false, true, SW, false, STRIDE, GROUPS>(a);
 }
 
 // ---- residual --------------------------------------------------------------------------
@@ -1304,7 +1337,9 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   Kern k;
   const size_t lds = 0;
   if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
-    k = sw ? k_step1<true> : k_step1<false>;
+    if (a.groups && a.chunk_stride) k = sw ? k_step1<true, true, true> : k_step1<false, true, true>;
+    else if (a.groups) k = sw ? k_step1<true, true> : k_step1<false, true>;
+    else k = sw ? k_step1<true> : k_step1<false>;
   } else if (a.groups) {
     if (a.chunk_stride) {
       if (a.fast_div) k = sw ? k_step<true, true, false, true, true> : k_step<true, false, false, true, true>;

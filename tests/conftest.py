@@ -51,14 +51,14 @@ def knob(lbm):
         lbm.tune(which, prev)
 
 
-@pytest.fixture(params=["4", "4g", "1"], ids=["4cells", "4groups", "1cell"])
+@pytest.fixture(params=["4", "4g", "1", "1g"], ids=["4cells", "4groups", "1cell", "1groups"])
 def cells_per_lane(request, knob, lbm):
     """Run a parity test through every stream-collide path: four cells per lane over whole
     chunks (the bandwidth path), four cells per lane over compact lists of active 4-cell groups
-    (sparse lattices; forced on every sparse chunk list), and one cell per lane (what small
-    lattices use by default)."""
+    (sparse lattices; forced on every sparse chunk list), one cell per lane over whole chunks
+    (what small lattices use by default) and one cell per lane over the group lists."""
     knob(lbm.TUNE_CELLS_PER_LANE, 4 if request.param.startswith("4") else 1)
-    knob(lbm.TUNE_GROUPS, 2 if request.param == "4g" else 1)
+    knob(lbm.TUNE_GROUPS, 2 if request.param.endswith("g") else 1)
     return 4 if request.param.startswith("4") else 1
 
 
