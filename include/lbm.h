@@ -173,9 +173,11 @@ typedef enum {
   LBM_TUNE_INJECT_RCCL_FAULT = 7, /* test hook: 1 = the next wait of an RCCL context (lbm_sync, a
                                    synchronising lbm_step, a read-out) sees a failed peer; the knob
                                    resets itself.  Exercises the abort path below. */
-  LBM_TUNE_GROUPS = 8,          /* 4-cell step kernel, sparse chunk lists: 0 (default) compact lists
-                                   of the active 4-cell groups (64 per wave) when the chunks' lanes
-                                   are under 3/4 busy, 1 never, 2 on every sparse list */
+  LBM_TUNE_GROUPS = 8,          /* sparse chunk lists: 0 (default) compact lists of the active 4-cell
+                                   groups when the chunks' lanes (one cell per lane: cells) are under
+                                   3/4 busy, 1 never, 2 on every sparse list.  With CELLS_PER_LANE 0
+                                   a list of at most 8192 x 64 groups runs one cell per lane (16
+                                   groups per wave), a longer one four (64 per wave) */
   LBM_TUNE_GROUP_SEGMENT = 9,   /* group lists: 1..64 groups per segment (default 8: one 128-B line);
                                    a segment with an active group enters the list whole, its idle
                                    groups load nothing */
@@ -290,9 +292,10 @@ int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_
 /* How the step kernel covers the whole-domain chunks (not a reference interface: diagnostics
  * for benchmarks and tests): cells_per_lane 1 or 4, main_blocks = its chunk workgroups,
  * grid_stride 1 when those loop over their XCD's chunks (LBM_TUNE_GRID_STRIDE), 2 when its
- * waves take compact lists of active 4-cell groups (LBM_TUNE_GROUPS); lane_fill = mean share
- * of chunk lanes (with groups: of a listed group's cells) with a cell to update.  Nullable
- * outputs. */
+ * waves take compact lists of active 4-cell groups (LBM_TUNE_GROUPS; 64 groups per wave with
+ * four cells per lane, 16 with one); lane_fill = mean share of chunk lanes (one cell per lane:
+ * of the chunks' cells; with groups: of a listed group's cells) with a cell to update.
+ * Nullable outputs. */
 int lbm_get_launch_shape(lbm_ctx* ctx, int* cells_per_lane, int* main_blocks, int* grid_stride, double* lane_fill);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (each stores its NEE
  * neighbours' values, producer side). */

@@ -383,9 +383,31 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMalloc(&r.chunks, sizeof(int) * r.nchunks));
     HIPCK(c, hipMemcpy(r.chunks, chunks.data(), sizeof(int) * r.nchunks, hipMemcpyHostToDevice));
   }
+  bool group1 = false;  // a sparse list too short for the 4-cell path: one-cell group list
   {
     const int cpl = g_tune[LBM_TUNE_CELLS_PER_LANE];  // A/B switch: 1 or 4 (0: by size)
     r.quarter = cpl ? (cpl == 1) : (r.nchunks <= kQuarterMaxChunks);
+    // The 4-cell path wants several rounds of resident waves (two per SIMD): a range of at
+    // most kQuarterMaxChunks waves runs one cell per lane (four per SIMD), and the same
+    // count decides for a sparse list that would take the 4-cell group list -- its waves are
+    // its active groups / 64.  The coronary tree (3.9k such waves): 58.8 -> 42.3 us per step
+    // one cell per lane; the upsampled bifurcation (15k) keeps four cells per lane (+2% the
+    // other way; profiles/r03_groups1_ab.log).
+    const int gm = g_tune[LBM_TUNE_GROUPS];
+    if (!cpl && !r.quarter && r.chunk0 < 0 && gm != 1) {
+      int64_t active = 0;
+      for (int ch : chunks)
+        for (int l = 0; l < 64; ++l) {
+          bool any = false;
+          for (int k = 0; k < 4; ++k) {
+            const int64_t cell = (int64_t)ch * kChunk + 4 * l + k;
+            any |= in(cell) && (t[cell] & kClassMask) == kFluid && !(t[cell] & kNeeAdj);
+          }
+          active += any;
+        }
+      const double fill4 = (double)active / (64.0 * (double)r.nchunks);
+      if ((gm == 2 || fill4 < 0.75) && (active + 63) / 64 <= kQuarterMaxChunks) r.quarter = group1 = true;
+    }
   }
   // 4-cell ranges: the NEE-adjacent cells go to NEE blocks, one per thread.  In a chunk wave
   // each would add two dependent load rounds (its NEE-link mask, then its neighbours' boundary
@@ -484,7 +506,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   {
     const int gm = g_tune[LBM_TUNE_GROUPS];
     const bool sparse = r.quarter ? r.lane_fill < kGroupFill1 : r.lane_masks && r.lane_fill < 0.75;
-    const bool want = gm == 2 || (gm == 0 && sparse);
+    const bool want = gm == 2 || (gm == 0 && (sparse || group1));
     if (r.nchunks && r.chunk0 < 0 && want) {
       // segments of seg groups (LBM_TUNE_GROUP_SEGMENT, default 8 = one 128-B line of a chunk
       // slice): a segment with an active group enters the list whole, its idle groups marked

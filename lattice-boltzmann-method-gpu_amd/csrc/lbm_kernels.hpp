@@ -147,7 +147,7 @@ int nee_waves_for(int n, double contiguous);
 int nee_grid(int n, int waves);
 int main_grid(int nchunks, bool quarter);
 constexpr int kQuarterMaxChunks = 8192;  // <= 128^3 cells: one cell per lane (latency-bound sizes)
-constexpr double kGroupFill1 = 0.0;        // one-cell ranges take the group list below this cell fill
+constexpr double kGroupFill1 = 0.75;       // one-cell ranges take the group list below this cell fill
 constexpr int kReduceBlocks = 256;
 // partial sums -> conv->s_local (deterministic: one block for up to 16384 partials, else
 // kReduceBlocks blocks sum fixed contiguous slices into scratch and one block sums those);

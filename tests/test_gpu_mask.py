@@ -216,3 +216,35 @@ def test_groups_bitwise(gpu, knob, case):
     assert np.array_equal(f1.view(np.uint32), f0.view(np.uint32)), case
     # per-block fp64 partials: the launch shape may move the residual's last bits (lbm.h)
     assert np.all(np.isfinite(h1)) and np.allclose(h1, h0, rtol=0, atol=2e-7), (h1, h0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["coronary", "bif"])
+def test_one_cell_groups_default_bitwise(gpu, knob, case):
+    """A sparse list with few active groups (the coronary tree; C4, whose 391 chunks are one-cell
+    size anyway) runs one cell per lane over the compact group list by default.  Forcing four
+    cells per lane over the same list, or one cell per lane over whole chunks, changes only
+    which lane updates which cell: populations bit for bit equal."""
+    from lbm_amd import cases
+
+    def build():
+        if case == "coronary":
+            return cases.coronary(cases.coronary_reference_vessel())[0]
+        return cases.bifurcation(1)[0]
+
+    def run(cpl, groups):
+        with gpu.tuned(gpu.TUNE_CELLS_PER_LANE, cpl), gpu.tuned(gpu.TUNE_GROUPS, groups):
+            lat = build()
+        shape = lat.launch_shape()
+        hist = lat.step(12)
+        f = lat.f()
+        lat.close()
+        return shape, f, hist
+
+    s0, f0, h0 = run(0, 0)
+    assert s0["cells_per_lane"] == 1 and s0["grid_stride"] == 2, s0
+    for cpl, groups, want in ((4, 2, (4, 2)), (1, 1, (1, 0))):
+        s, f, h = run(cpl, groups)
+        assert (s["cells_per_lane"], s["grid_stride"]) == want, (cpl, groups, s)
+        assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), (case, cpl, groups)
+        assert np.all(np.isfinite(h)) and np.allclose(h, h0, rtol=0, atol=2e-7), (h, h0)
