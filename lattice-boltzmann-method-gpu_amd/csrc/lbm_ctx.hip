@@ -107,6 +107,8 @@ struct lbm_ctx {
   bool conv_enabled = false;
   bool halo_primed = false;
   int64_t n_box = 0, n_fluid = 0, n_slow = 0, n_wall_adj = 0;
+  bool bc_uniform = false;  // every NEE cell holds the record bc_const (fill_main_args)
+  float4 bc_const{};
   float tau = 0.f, omc = 0.f;
   bool fast_div = false;  // tau verified for the 3-VALU correctly rounded division
   unsigned long long* retried = nullptr;  // device: 4-cell waves that took the exact division
@@ -313,6 +315,8 @@ void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
   a.exact_waves = c->retried;
   a.omc = c->omc;
   a.swap = c->L.swap;
+  a.bc_uniform = c->bc_uniform ? 1 : 0;
+  a.bc_const = c->bc_const;
 }
 
 // one step of a range from buffer srcbuf into srcbuf ^ 1
@@ -912,6 +916,28 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
           }
         }
     c->n_fluid = nf;
+    {  // one boundary record for every NEE cell (the cavity's lid): the kernels take it from
+       // their arguments instead of loading it
+      int64_t ref = -1;
+      for (int64_t k = 0; k < L.ncell && ref < 0; ++k)
+        if ((t[k] & kClassMask) == kNee) ref = k;
+      if (ref >= 0) {
+        unsigned* flag = nullptr;
+        unsigned differs = 1;
+        float rec[4];
+        CK(hipMalloc(&flag, sizeof(unsigned)));
+        hipError_t e = hipMemsetAsync(flag, 0, sizeof(unsigned), c->s_comp);
+        if (e == hipSuccess) e = launch_bc_uniform(c->type, c->rho, c->ux, c->uy, c->uz, L.ncell, ref, flag, c->s_comp);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->s_comp);
+        if (e == hipSuccess) e = hipMemcpy(&differs, flag, sizeof(unsigned), hipMemcpyDeviceToHost);
+        const float* arr[4] = {c->rho, c->ux, c->uy, c->uz};
+        for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipMemcpy(&rec[k], arr[k] + ref, sizeof(float), hipMemcpyDeviceToHost);
+        (void)hipFree(flag);
+        CK(e);
+        c->bc_uniform = differs == 0;
+        c->bc_const = make_float4(rec[0], rec[1], rec[2], rec[3]);
+      }
+    }
     const int64_t P = L.plane, nz = d.nz;
     if (build_range(c, c->whole, P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
     if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);

@@ -298,6 +298,7 @@ __device__ __forceinline__ float4 bc_next(const MainArgs& a, int64_t c, uint32_t
 }
 template <bool SW>
 __device__ __forceinline__ BcSlots nee_prefetch(const MainArgs& a, int64_t c, uint32_t nl) {
+  if (a.bc_uniform) return BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const};
   BcSlots b;
   uint32_t rest = nl;
   b.s0 = bc_next<SW>(a, c, rest);
@@ -612,7 +613,8 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const int64_t c = a.cells[i];
   const uint32_t nl = a.cell_nl[i];
   const float4* r = a.nee_bc + (int64_t)i * kNeeSlots;
-  const BcSlots bc{r[0], r[1], r[2], r[3], r[4]};
+  const BcSlots bc = a.bc_uniform ? BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const}
+                                  : BcSlots{r[0], r[1], r[2], r[3], r[4]};
   const uint32_t links = a.links[c];
   float f[kQ];
   pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
@@ -1485,6 +1487,19 @@ hipError_t launch_probe_fill(void* dst, int64_t n4, hipStream_t s) {
   return hipGetLastError();
 }
 
+__global__ void k_bc_uniform(const uint8_t* __restrict__ type, const float* __restrict__ rho,
+                             const float* __restrict__ ux, const float* __restrict__ uy,
+                             const float* __restrict__ uz, int64_t n, int64_t ref, unsigned* differs) {
+  const uint32_t r0 = __float_as_uint(rho[ref]), r1 = __float_as_uint(ux[ref]), r2 = __float_as_uint(uy[ref]),
+                 r3 = __float_as_uint(uz[ref]);
+  bool d = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if ((type[i] & kClassMask) == kNee)
+      d |= __float_as_uint(rho[i]) != r0 || __float_as_uint(ux[i]) != r1 || __float_as_uint(uy[i]) != r2 ||
+           __float_as_uint(uz[i]) != r3;
+  if (d) atomicOr(differs, 1u);
+}
+
 template <bool SW>
 __global__ void k_nee_gather(const int* __restrict__ cells, const uint32_t* __restrict__ nl,
                              const float* __restrict__ rho, const float* __restrict__ ux,
@@ -1504,6 +1519,14 @@ __global__ void k_nee_gather(const int* __restrict__ cells, const uint32_t* __re
     }
     out[(int64_t)i * kNeeSlots + j] = v;
   }
+}
+
+hipError_t launch_bc_uniform(const uint8_t* type, const float* rho, const float* ux, const float* uy,
+                             const float* uz, int64_t ncell, int64_t ref, unsigned* differs, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(4096, (ncell + 255) / 256);
+  hipLaunchKernelGGL(k_bc_uniform, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(256), 0, s, type, rho, ux, uy,
+                     uz, ncell, ref, differs);
+  return hipGetLastError();
 }
 
 hipError_t launch_nee_gather(const int* cells, const uint32_t* nl, const float* rho, const float* ux,

@@ -61,6 +61,8 @@ struct MainArgs {
   const float* rho; const float* ux; const float* uy; const float* uz;  // NEE data at NEE cells:
                         // rho_bc or NaN (rho of the fluid neighbour), u_bc or NaN (pressure
                         // boundary: u of the fluid neighbour)
+  float4 bc_const;      // with bc_uniform = 1: every NEE cell's record (rho, ux, uy, uz), bit for
+  int bc_uniform;       // bit -- the cavity's lid -- so no NEE cell loads one
   double* partial;      // one per block
   const int* chunks;    // active chunk ids
   int chunk0;           // >= 0: they are chunk0, chunk0 + 1, ... (box lattices) -- no list load,
@@ -138,6 +140,9 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s);
 // with more (edges and corners of several faces) loads the rest where they are used
 constexpr int kNeeSlots = 5;
 // nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of nl[i]
+// 1 into *differs when some NEE cell's record (rho, ux, uy, uz) differs bitwise from cell ref's
+hipError_t launch_bc_uniform(const uint8_t* type, const float* rho, const float* ux, const float* uy,
+                             const float* uz, int64_t ncell, int64_t ref, unsigned* differs, hipStream_t s);
 hipError_t launch_nee_gather(const int* cells, const uint32_t* nl, const float* rho, const float* ux,
                              const float* uy, const float* uz, float4* nee_bc, int n, int pitch, int64_t plane,
                              int swap, hipStream_t s);
