@@ -107,21 +107,41 @@ def c5_one_gpu(dev: int, steps: int = 10):
             "setup_s": round(setup, 1)}
 
 
-def timed_mlups(lat, cells: dict, steps: int, warm: int = 20):
+def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
+    """Wall-clock MLUPS over `steps` steps, then k_step's own roofline from HIP events over a
+    second, profiled run: algorithmic bytes (152 B x fluid cells) / mean launch time against 8 TB/s,
+    with the HBM bytes per launch rocprofv3 counted for this lattice (profiles/pmc_traffic.json,
+    tools/pmc_lattices.sh) when present."""
     lay = lat.layout()
     shape = lat.launch_shape()
+    algo = lat.counts()["algo_bytes_per_step"]
     lat.step(warm, history=False)
     lat.sync()
     t = time.perf_counter()
     lat.step(steps, history=False)
     lat.sync()
     dt = time.perf_counter() - t
+    lat.profile(True)
+    lat.step(min(steps, 200), history=False)
+    st = lat.stats()
     lat.close()
     out = {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
     out["rows_along"] = "xy"[lay["row_axis"] - 1]
     out["active_chunks"] = lay["active_chunks"]
     out["cells_per_lane"] = shape["cells_per_lane"]
     out["grid_stride"] = shape["grid_stride"]
+    out["lane_fill"] = shape["lane_fill"]
+    kms = st["step_kernel_ms"] / max(1, st["step_kernel_launches"])
+    if kms > 0:
+        gbs = algo / (kms * 1e-3) / 1e9
+        rl = {"avg_kernel_us": round(kms * 1e3, 2), "algo_bytes_per_launch": int(algo),
+              "achieved": round(gbs, 1), "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None}
+        pmc = pmc_traffic(name) if name else None
+        if pmc:
+            rl["traffic"] = pmc["bytes_per_launch"]
+            rl["traffic_over_algo"] = pmc.get("traffic_over_algo")
+            rl["traffic_source"] = f"profiles/pmc_traffic.json ({pmc.get('tag')}, tools/pmc_lattices.sh)"
+        out["roofline"] = rl
     return out
 
 
@@ -132,25 +152,27 @@ def config_lines(dev: int):
     out = {}
     lat, geo = cases.poiseuille(128, 512, 128, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
-    out["poiseuille_128x512x128 (C3)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
+    k = "poiseuille_128x512x128 (C3)"
+    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200, name=k)
     # the same lattice on the x-row layout (lbm_desc.row_axis = 1), for comparison
     with lbm_amd.tuned(lbm_amd.TUNE_ROW_AXIS, 1):
         lat, geo = cases.poiseuille(128, 512, 128, device=dev)
     out["poiseuille_128x512x128 (C3), x rows"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
     lat, geo, _, _ = cases.bifurcation(1, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
-    out["bifurcation_64x83x32 (C4)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 2000)
+    k = "bifurcation_64x83x32 (C4)"
+    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 2000, name=k)
     # SURVEY 8(d) C4's bandwidth-relevant sparse number: the shipped mask upsampled 4x per axis
     lat, raw = cases.bifurcation_upsampled(4, device=dev)
     nl, _ = lbm_amd.index_transform(lat.geo())
-    out["bifurcation_x4_256x332x128 (C4 upsampled)"] = timed_mlups(lat, {"mlups_box": raw.size,
-                                                                         "mlups_nlattice": nl}, 200)
+    k = "bifurcation_x4_256x332x128 (C4 upsampled)"
+    out[k] = timed_mlups(lat, {"mlups_box": raw.size, "mlups_nlattice": nl}, 200, name=k)
     # coronary.cu's 291 x 291 x 372 box with its five open ends on a synthetic vessel tree (the
     # reference's geo.txt is not shipped): a sparse lattice, 2.5 % of the box stored
     lat, geo = cases.coronary(cases.coronary_reference_vessel(), device=dev)
     nl, _ = lbm_amd.index_transform(geo)
-    out["coronary_291x291x372 (synthetic vessel)"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl},
-                                                                 1000)
+    k = "coronary_291x291x372 (synthetic vessel)"
+    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 1000, name=k)
     return out
 
 
