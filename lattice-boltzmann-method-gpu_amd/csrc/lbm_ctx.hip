@@ -61,7 +61,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   uint32_t* cell_nl = nullptr;  // their NEE-link masks
   float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
-  int* groups = nullptr;  // 4-cell path, sparse ranges: compact list of active 4-cell groups
+  int* groups = nullptr;  // sparse ranges: compact list of active 4-cell groups (both paths)
   int64_t ngroups = 0;
   double group_fill = 0.0;  // mean share of a listed group's cells the wave updates
   unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
@@ -504,7 +504,8 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // Compact 4-cell groups (LBM_TUNE_GROUPS): on a sparse chunk list whose lanes are mostly idle
   // (vessel trees), the wave's VALU work is the same whether a lane holds a cell or not, so
   // idle lanes cost issue time.  The groups holding a cell to update go into one compact list
-  // in storage order, 64 per wave; runs of neighbouring groups keep their loads and stores
+  // in storage order, 64 per 4-cell wave (16 per one-cell wave); runs of neighbouring groups
+  // keep their loads and stores
   // contiguous, and a group whose list neighbour is not its row neighbour loads its x-edge
   // cells itself (pull_issue).
   {

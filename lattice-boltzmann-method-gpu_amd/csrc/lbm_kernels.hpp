@@ -71,9 +71,10 @@ struct MainArgs {
   const unsigned long long* lane_masks;  // nullable (4-cell path): per chunk of the list, bit l set when
                         // lane l (cells 4l .. 4l+3) or a neighbouring lane holds a cell the chunk
                         // wave updates; the other lanes load nothing (sparse lattices)
-  const int* groups;    // nullable (4-cell path, sparse lists): compact list of active 4-cell groups
-                        // (first cell id of each, a multiple of 4, storage order); when set,
-                        // wave w takes entries 64 w .. 64 w + 63, one group per lane
+  const int* groups;    // nullable (sparse lists): compact list of active 4-cell groups (first cell
+                        // id of each, a multiple of 4, bit 0 set for an idle group of a segment,
+                        // storage order); 4-cell waves take 64 entries (one per lane), one-cell
+                        // waves 16 (four lanes per entry)
   int64_t ngroups;
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
   int chunk_stride;     // 1: each XCD's chunk waves loop over its eighth of the chunk list
