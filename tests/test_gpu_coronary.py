@@ -23,6 +23,7 @@ def _oracle(oracle, geo):
     from lbm_amd import cases
     o = oracle.Oracle(oracle.GENERIC, geo, cases.CORONARY_TAU, bcs=cases.coronary_bc_codes())
     o.initialize_coronary()
+    o.residual_fp64(True)  # liblbm's summation (assert_residuals)
     return o
 
 
