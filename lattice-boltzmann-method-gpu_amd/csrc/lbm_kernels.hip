@@ -217,6 +217,8 @@ struct Pref {  // RN(rho / 3), RN(rho / 18), RN(rho / 36)
   __device__ __forceinline__ explicit Pref(float r)
       : p3(fast_quot(r, 3.0f, 1.0f / 3.0f)), p18(fast_quot(r, 18.0f, 1.0f / 18.0f)),
         p36(fast_quot(r, 36.0f, 1.0f / 36.0f)) {}
+  __device__ __forceinline__ Pref(float a, float b, float c) : p3(a), p18(b), p36(c) {}
+  __device__ __forceinline__ static Pref exact(float r) { return Pref(r / 3.0f, r / 18.0f, r / 36.0f); }
   template <int Q>
   __device__ __forceinline__ float of() const {
     return FeqW<Q>::d == 3.0f ? p3 : FeqW<Q>::d == 18.0f ? p18 : p36;
@@ -309,15 +311,20 @@ __device__ __forceinline__ BcSlots nee_prefetch(const MainArgs& a, int64_t c, ui
   return b;
 }
 
+// pre: RN(r / w_Q's divisor), the fluid cell's equilibrium prefactor from its relaxation, so
+// feq<Q>(r, ..) = feq_pre<Q>(pre, ..) bit for bit and neither equilibrium divides again
 template <int Q>
-__device__ __forceinline__ float nee_value(float fq, float4 b, float r, float ux, float uy, float uz, float omc) {
+__device__ __forceinline__ float nee_value(float fq, float4 b, float r, float ux, float uy, float uz, float omc,
+                                           float pre) {
   float rb = b.x, bx = b.y, by = b.z, bz = b.w;
   if (__builtin_isnan(bx)) {  // pressure boundary: u_bc = u of the fluid neighbour
     bx = ux; by = uy; bz = uz;
   }
-  if (__builtin_isnan(rb)) rb = r;  // velocity boundary: rho_bc = rho of the fluid neighbour
-  const float e_bc = feq_bc<Q>(rb, bx, by, bz);
-  const float e_nb = feq<Q>(r, ux, uy, uz);
+  const bool rn = __builtin_isnan(rb);  // velocity boundary: rho_bc = rho of the fluid neighbour
+  float e_bc;
+  if constexpr (Q == 14) e_bc = feq_bc<14>(rn ? r : rb, bx, by, bz);  // its own fp32 form
+  else e_bc = feq_pre<Q>(rn ? pre : rb / FeqW<Q>::d, bx, by, bz);
+  const float e_nb = feq_pre<Q>(pre, ux, uy, uz);
   return e_bc + (fq - e_nb) * omc;
 }
 
@@ -332,7 +339,7 @@ struct Post1 {
 template <int Q, bool SW, class Src>
 __device__ __forceinline__ void nee_store_q(const MainArgs& a, int64_t c, uint32_t nl, float4 b0, float4 b1, float4 b2,
                                             float4 b3, float4 b4, const Src& src, float r, float ux, float uy,
-                                            float uz) {
+                                            float uz, const Pref& p) {
   if constexpr (Q > 0) {
     if (nl & (1u << Q)) {  // divergent only where a wave mixes faces (edges, corners)
       const int k = __builtin_popcount(nl & ((1u << Q) - 1u));  // Q's slot
@@ -341,7 +348,7 @@ __device__ __forceinline__ void nee_store_q(const MainArgs& a, int64_t c, uint32
       if (k >= kNeeSlots) b = bc_at(a, nb);
       else b = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : k == 3 ? b3 : b4;
       const float fq = src.template post<Q>(a, r, ux, uy, uz);
-      a.dst[aidx(nb, Q)] = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc);
+      a.dst[aidx(nb, Q)] = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc, p.template of<Q>());
     }
   }
 }
@@ -350,12 +357,13 @@ __device__ __forceinline__ void opaque(float4& v) { asm volatile("" : "+v"(v.x),
 
 template <bool SW, class Src, int... Qs>
 __device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint32_t nl, BcSlots bc, const Src& src,
-                                              float r, float ux, float uy, float uz, std::integer_sequence<int, Qs...>) {
+                                              float r, float ux, float uy, float uz, const Pref& p,
+                                              std::integer_sequence<int, Qs...>) {
   // plain registers from here on: otherwise the slot selections below fold into one load at
   // a variable offset, and the records go through scratch
   float4 b0 = bc.s0, b1 = bc.s1, b2 = bc.s2, b3 = bc.s3, b4 = bc.s4;
   opaque(b0); opaque(b1); opaque(b2); opaque(b3); opaque(b4);
-  (nee_store_q<Qs, SW>(a, c, nl, b0, b1, b2, b3, b4, src, r, ux, uy, uz), ...);
+  (nee_store_q<Qs, SW>(a, c, nl, b0, b1, b2, b3, b4, src, r, ux, uy, uz, p), ...);
 }
 
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
@@ -514,10 +522,15 @@ __device__ __forceinline__ bool fast_div_ok1(const float* f, float r, float ux, 
 }
 // one cell's relaxation: the fast quotient when tau is verified and every active lane of
 // the wave lies in its domain (a wave-uniform choice: the lanes stay together), else exact
-__device__ __forceinline__ void relax1(float* f, const MainArgs& a, float r, float ux, float uy, float uz) {
+// returns the equilibrium prefactors RN(r / 3), RN(r / 18), RN(r / 36) (for the NEE values)
+__device__ __forceinline__ Pref relax1(float* f, const MainArgs& a, float r, float ux, float uy, float uz) {
   const bool ok = fast_div_ok1(f, r, ux, uy, uz);
-  if (a.tau_fast && __all(ok)) fix_relax_fast_all(f, a.tau, a.tau_rcp, r, ux, uy, uz, AllQ{});
-  else fix_relax_all(f, a.tau, r, ux, uy, uz, AllQ{});
+  if (a.tau_fast && __all(ok)) {
+    fix_relax_fast_all(f, a.tau, a.tau_rcp, r, ux, uy, uz, AllQ{});
+    return Pref(r);
+  }
+  fix_relax_all(f, a.tau, r, ux, uy, uz, AllQ{});
+  return Pref::exact(r);
 }
 template <bool SW, int... Qs>
 __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m,
@@ -566,8 +579,8 @@ __device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, ui
   const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  relax1(f, a, rho, ux, uy, uz);
-  if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, AllQ{});
+  const Pref pre = relax1(f, a, rho, ux, uy, uz);
+  if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
   fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
@@ -624,8 +637,8 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  relax1(f, a, rho, ux, uy, uz);
-  nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, AllQ{});
+  const Pref pre = relax1(f, a, rho, ux, uy, uz);
+  nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
   fix_store_all<SW>(f, a.dst, c, links, a.pitch, a.plane, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
