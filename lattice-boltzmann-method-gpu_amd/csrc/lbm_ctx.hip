@@ -63,6 +63,8 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
   int* groups = nullptr;  // sparse ranges: compact list of active 4-cell groups (both paths)
   int64_t ngroups = 0;
+  int* group_bc = nullptr;         // one-cell group lists: per entry, its NEE records' index or -1
+  float4* group_rec = nullptr;     // kNeeSlots records per cell of the groups with NEE-adjacent cells
   double group_fill = 0.0;  // mean share of a listed group's cells the wave updates
   unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
   double* part = nullptr; // one |u| partial per block (NEE blocks, then chunk blocks)
@@ -329,6 +331,8 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
   a.groups = r.groups;
   a.ngroups = r.ngroups;
+  a.group_bc = r.group_bc;
+  a.group_rec = r.group_rec;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
@@ -420,24 +424,27 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // arithmetic).
   double contig = 1.0;
   if (r.quarter) cells.clear();
+  // the NEE-link mask of k_flag_fluid: q crosses the NEE neighbour's face (e_q . n == 1)
+  int64_t off[kQ];
+  for (int q = 0; q < kQ; ++q) {
+    const int s0 = c->L.swap ? kEy[q] : kEx[q], s1 = c->L.swap ? kEx[q] : kEy[q];
+    off[q] = s0 + (int64_t)s1 * c->L.pitch + (int64_t)kEz[q] * c->L.plane;
+  }
+  auto nl_of = [&](int64_t cell) {
+    uint32_t m = 0;
+    for (int q = 1; q < kQ; ++q) {
+      const int64_t nb = cell - off[q];
+      if (nb < 0 || nb >= (int64_t)t.size() || (t[nb] & kClassMask) != kNee) continue;
+      const int fb = (kEx[q] == 1 ? 1 : 0) | (kEx[q] == -1 ? 2 : 0) | (kEy[q] == 1 ? 4 : 0) |
+                     (kEy[q] == -1 ? 8 : 0) | (kEz[q] == 1 ? 16 : 0) | (kEz[q] == -1 ? 32 : 0);
+      if ((fb >> nee_face(t[nb])) & 1) m |= 1u << q;
+    }
+    return m;
+  };
   r.n_nee = (int)cells.size();
   if (r.n_nee) {
     std::vector<uint32_t> nl(cells.size());
-    {  // the NEE-link masks of k_flag_fluid: q crosses the NEE neighbour's face (e_q . n == 1)
-      int64_t off[kQ];
-      for (int q = 0; q < kQ; ++q) {
-        const int s0 = c->L.swap ? kEy[q] : kEx[q], s1 = c->L.swap ? kEx[q] : kEy[q];
-        off[q] = s0 + (int64_t)s1 * c->L.pitch + (int64_t)kEz[q] * c->L.plane;
-      }
-      for (size_t i = 0; i < cells.size(); ++i)
-        for (int q = 1; q < kQ; ++q) {
-          const int64_t nb = cells[i] - off[q];
-          if (nb < 0 || nb >= (int64_t)t.size() || (t[nb] & kClassMask) != kNee) continue;
-          const int fb = (kEx[q] == 1 ? 1 : 0) | (kEx[q] == -1 ? 2 : 0) | (kEy[q] == 1 ? 4 : 0) |
-                         (kEy[q] == -1 ? 8 : 0) | (kEz[q] == 1 ? 16 : 0) | (kEz[q] == -1 ? 32 : 0);
-          if ((fb >> nee_face(t[nb])) & 1) nl[i] |= 1u << q;
-        }
-    }
+    for (size_t i = 0; i < cells.size(); ++i) nl[i] = nl_of(cells[i]);
     // group cells with the same directions (inlet / outlet / lid faces, edges) so that the
     // lanes of a wave take the same branches; cell order within a group
     std::vector<size_t> perm(cells.size());
@@ -540,6 +547,40 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         HIPCK(c, hipMalloc(&r.groups, sizeof(int) * gl.size()));
         HIPCK(c, hipMemcpy(r.groups, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice));
       }
+      // one-cell waves: the boundary records of the groups holding NEE-adjacent cells, gathered
+      // once and indexed by list entry (process_group_cell1 loads them with the pulls)
+      if (r.quarter && r.ngroups && !c->bc_uniform) {
+        std::vector<int> gbc(gl.size(), -1), gcells;
+        std::vector<uint32_t> gnl;
+        auto nee_adj = [&](int64_t k) { return in(k) && (t[k] & kClassMask) == kFluid && (t[k] & kNeeAdj); };
+        int nrec = 0;
+        for (size_t i = 0; i < gl.size(); ++i) {
+          if (gl[i] & 1) continue;
+          const int64_t g = gl[i];
+          if (!(nee_adj(g) || nee_adj(g + 1) || nee_adj(g + 2) || nee_adj(g + 3))) continue;
+          gbc[i] = nrec++;
+          for (int64_t j = g; j < g + 4; ++j) {
+            gcells.push_back((int)j);
+            gnl.push_back(nee_adj(j) ? nl_of(j) : 0u);
+          }
+        }
+        if (nrec) {
+          int* dc = nullptr;
+          uint32_t* dn = nullptr;
+          HIPCK(c, hipMalloc(&r.group_bc, sizeof(int) * gbc.size()));
+          HIPCK(c, hipMemcpy(r.group_bc, gbc.data(), sizeof(int) * gbc.size(), hipMemcpyHostToDevice));
+          HIPCK(c, hipMalloc(&r.group_rec, sizeof(float4) * kNeeSlots * gcells.size()));
+          HIPCK(c, hipMalloc(&dc, sizeof(int) * gcells.size()));
+          HIPCK(c, hipMalloc(&dn, sizeof(uint32_t) * gnl.size()));
+          HIPCK(c, hipMemcpy(dc, gcells.data(), sizeof(int) * gcells.size(), hipMemcpyHostToDevice));
+          HIPCK(c, hipMemcpy(dn, gnl.data(), sizeof(uint32_t) * gnl.size(), hipMemcpyHostToDevice));
+          HIPCK(c, launch_nee_gather(dc, dn, c->rho, c->ux, c->uy, c->uz, r.group_rec, (int)gcells.size(),
+                                     c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
+          HIPCK(c, hipStreamSynchronize(c->s_comp));
+          (void)hipFree(dc);
+          (void)hipFree(dn);
+        }
+      }
       const int64_t waves = (r.ngroups + (r.quarter ? 15 : 63)) / (r.quarter ? 16 : 64);
       r.main_blocks = waves ? (int)std::max<int64_t>(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
     }
@@ -572,6 +613,8 @@ void free_range(Range& r) {
   if (r.chunks) (void)hipFree(r.chunks);
   if (r.lane_masks) (void)hipFree(r.lane_masks);
   if (r.groups) (void)hipFree(r.groups);
+  if (r.group_bc) (void)hipFree(r.group_bc);
+  if (r.group_rec) (void)hipFree(r.group_rec);
   if (r.cells) (void)hipFree(r.cells);
   if (r.cell_nl) (void)hipFree(r.cell_nl);
   if (r.nee_bc) (void)hipFree(r.nee_bc);

@@ -564,15 +564,17 @@ __device__ __forceinline__ void pull1w_all(float* f, const float* __restrict__ s
 }
 
 // one cell's collision and stores once its pulls, type byte and link masks are in
-template <bool SW>
+template <bool SW, bool PRE_BC = false>
 __device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, uint8_t t, uint32_t links, uint32_t nl,
-                                                float* f) {
+                                                float* f, BcSlots pre_bc = BcSlots{}) {
   const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid;
   if (!in) return 0.0;
   // NEE-adjacent: the boundary data goes out now and arrives under the arithmetic below
+  // (PRE_BC: already loaded with the pulls)
   const bool nee = (t & kNeeAdj) != 0;
   BcSlots bc{};
-  if (nee) bc = nee_prefetch<SW>(a, c, nl);
+  if constexpr (PRE_BC) bc = pre_bc;
+  else if (nee) bc = nee_prefetch<SW>(a, c, nl);
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
@@ -605,7 +607,8 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, i
 template <bool SW>
 __device__ __forceinline__ double process_group_cell1(const MainArgs& a, int64_t w, int lane) {
   const int64_t gi = w * 16 + (lane >> 2);
-  const int e = a.groups[gi < a.ngroups ? gi : w * 16];
+  const int64_t gs = gi < a.ngroups ? gi : w * 16;
+  const int e = a.groups[gs];
   const bool need = gi < a.ngroups && !(e & 1);
   const int64_t c = (int64_t)(e & ~3) + (lane & 3);
   const uint8_t t = a.type[c];
@@ -613,7 +616,18 @@ __device__ __forceinline__ double process_group_cell1(const MainArgs& a, int64_t
   const uint32_t nl = a.nlinks[c];
   float f[kQ];
   pull1w_all<SW>(f, a.src, c >> 8, (int)(c & (kChunk - 1)), a.pitch, a.plane, AllQ{});  // per-lane chunk base
-  return collide_cell1<SW>(a, c, need ? t : (uint8_t)0, links, nl, f);
+  // the boundary records are indexed by the list entry, so they go out with the pulls instead
+  // of a round trip after the NEE-link mask (group_bc is null when the list holds no
+  // NEE-adjacent cell or every record is bc_const)
+  const int gb = a.group_bc ? a.group_bc[gs] : -1;
+  BcSlots bc{};
+  if (a.bc_uniform) {
+    bc = BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const};
+  } else if (gb >= 0) {
+    const float4* r = a.group_rec + ((int64_t)gb * 4 + (lane & 3)) * kNeeSlots;
+    bc = BcSlots{r[0], r[1], r[2], r[3], r[4]};
+  }
+  return collide_cell1<SW, true>(a, c, need ? t : (uint8_t)0, links, nl, f, bc);
 }
 
 // One NEE-adjacent fluid cell of a 4-cell range (NEE blocks, one per thread; the chunk waves

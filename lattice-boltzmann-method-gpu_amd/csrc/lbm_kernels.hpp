@@ -76,6 +76,10 @@ struct MainArgs {
                         // storage order); 4-cell waves take 64 entries (one per lane), one-cell
                         // waves 16 (four lanes per entry)
   int64_t ngroups;
+  const int* group_bc;        // nullable (one-cell group lists with NEE-adjacent cells, boundary
+                              // data not uniform): per list entry, the index of its 4 cells'
+                              // records in group_rec, or -1
+  const float4* group_rec;    // kNeeSlots records per cell of those groups (nee_prefetch's order)
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
   int chunk_stride;     // 1: each XCD's chunk waves loop over its eighth of the chunk list
                         // (lane-mask ranges only: k_step<..., MASK, STRIDE>)
