@@ -532,6 +532,47 @@ __device__ __forceinline__ Pref relax1(float* f, const MainArgs& a, float r, flo
   fix_relax_all(f, a.tau, r, ux, uy, uz, AllQ{});
   return Pref::exact(r);
 }
+// The fast relaxation with the NEE stores fused in (waves holding NEE-adjacent cells): slot Q
+// of the NEE neighbour c - e_Q is written as soon as f_Q is relaxed, from the same feq_Q (the
+// neighbour's e_nb) -- no second equilibrium per direction, nothing kept alive for later.
+template <int Q, bool SW>
+__device__ __forceinline__ void relax_nee_q(float* f, const MainArgs& a, const Pref& p, float r, float ux, float uy,
+                                            float uz, int64_t c, uint32_t nl, float4 b0, float4 b1, float4 b2,
+                                            float4 b3, float4 b4) {
+  const float pre = p.template of<Q>();
+  const float fe = feq_pre<Q>(pre, ux, uy, uz);
+  const float x = f[Q] - fe;
+  const float q0 = x * a.tau_rcp;
+  f[Q] = f[Q] - __builtin_fmaf(__builtin_fmaf(-q0, a.tau, x), a.tau_rcp, q0);
+  if constexpr (Q > 0) {
+    if (nl & (1u << Q)) {
+      const int k = __builtin_popcount(nl & ((1u << Q) - 1u));
+      const int64_t nb = c - cell_off<Q, SW>(a.pitch, a.plane);
+      float4 b;
+      if (k >= kNeeSlots) b = bc_at(a, nb);
+      else b = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : k == 3 ? b3 : b4;
+      float rb = b.x, bx = b.y, by = b.z, bz = b.w;
+      if (__builtin_isnan(bx)) {
+        bx = ux; by = uy; bz = uz;
+      }
+      const bool rn = __builtin_isnan(rb);
+      float e_bc;
+      if constexpr (Q == 14) e_bc = feq_bc<14>(rn ? r : rb, bx, by, bz);
+      else e_bc = feq_pre<Q>(rn ? pre : rb / FeqW<Q>::d, bx, by, bz);
+      a.dst[aidx(nb, Q)] = e_bc + (f[Q] - fe) * a.omc;
+    }
+  }
+}
+template <bool SW, int... Qs>
+__device__ __forceinline__ void relax_nee_fast_all(float* f, const MainArgs& a, float r, float ux, float uy, float uz,
+                                                   int64_t c, uint32_t nl, BcSlots bc,
+                                                   std::integer_sequence<int, Qs...>) {
+  const Pref p(r);
+  float4 b0 = bc.s0, b1 = bc.s1, b2 = bc.s2, b3 = bc.s3, b4 = bc.s4;
+  opaque(b0); opaque(b1); opaque(b2); opaque(b3); opaque(b4);
+  (relax_nee_q<Qs, SW>(f, a, p, r, ux, uy, uz, c, nl, b0, b1, b2, b3, b4), ...);
+}
+
 template <bool SW, int... Qs>
 __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m,
                                               int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
@@ -581,8 +622,13 @@ __device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, ui
   const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
-  const Pref pre = relax1(f, a, rho, ux, uy, uz);
-  if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
+  if (__any(nee) && a.tau_fast && __all(fast_div_ok1(f, rho, ux, uy, uz))) {
+    // (uniform) NEE values fused into the fast relaxation; nl = 0 on the other lanes
+    relax_nee_fast_all<SW>(f, a, rho, ux, uy, uz, c, nee ? nl : 0u, bc, AllQ{});
+  } else {
+    const Pref pre = relax1(f, a, rho, ux, uy, uz);
+    if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
+  }
   fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
