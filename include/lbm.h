@@ -18,7 +18,8 @@
  * one opaque context owns the device buffers of one lattice (or one z-slab of it),
  * and lbm_step() performs all of the above for n steps: a fused pull-stream +
  * collide kernel with wall bounce-back and non-equilibrium-extrapolation
- * boundaries evaluated by mask on the consumer side, a fused |u| reduction, a
+ * boundaries evaluated by mask and stored by each boundary slot's fluid neighbour
+ * right after its collision (producer side), a fused |u| reduction, a
  * device-side residual/convergence finisher, and (for slabs) the +-z halo exchange
  * over RCCL.  All pointers in these signatures are plain host pointers; no HIP or
  * torch types cross the boundary.  Every function returns LBM_OK (0) or a negative
