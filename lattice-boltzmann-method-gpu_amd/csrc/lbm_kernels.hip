@@ -368,7 +368,7 @@ __device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint
 
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
-//        branch) the exact division, counted in exact_waves.  Both paths cost 216-220 VGPRs
+//        branch) the exact division, counted in exact_waves.  Both paths cost 210-218 VGPRs
 //        against 170 for one -- no occupancy change: either way two waves per SIMD.
 template <bool FAST, bool SW, bool MASK, bool GROUPS = false>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
@@ -801,7 +801,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
   if (threadIdx.x == 0) a.partial[slot] = s;
 }
 
-// 4 cells per lane (big lattices): two waves per SIMD (216-220 VGPRs); MASK: the range has
+// 4 cells per lane (big lattices): two waves per SIMD (210-252 VGPRs); MASK: the range has
 // lane masks (sparse chunk lists)
 template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
