@@ -369,7 +369,8 @@ __device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
 //        branch) the exact division, counted in exact_waves.  Both paths cost 210-218 VGPRs
-//        against 170 for one -- no occupancy change: either way two waves per SIMD.
+//        (two waves per SIMD) against 162-166 for the exact one alone, whose three waves per
+//        SIMD ran slower (profiles/r03_fast3_ab.log).
 template <bool FAST, bool SW, bool MASK, bool GROUPS = false>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
   double acc = 0.0;
