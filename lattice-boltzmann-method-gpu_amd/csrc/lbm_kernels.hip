@@ -186,6 +186,49 @@ __device__ __forceinline__ void bb_store_cell(float* __restrict__ dst, int64_t c
   }
 #undef LBM_BB_CASE
 }
+// Whole-group bounce-back stores.  For direction q with along-row offset s (SDir x) the walls
+// c + j - e_q of a lane's cells j = 0..3 are cells c - ro + j - s: for s = 0 the aligned group
+// G = c - ro itself; for s = +1 (-1) G's slots 0..2 (1..3) with the neighbouring lane's cell 0
+// (cell 3) supplying the last (first) one.  A lane whose cells -- and that neighbour -- all link
+// q writes G in one 16-B store of post-collision f_opp(q) values, instead of four scattered
+// floats: the same slots with the same values, each still written once, by its one consumer.
+template <bool SW, int S>
+constexpr uint32_t links_along() {  // directions whose along-row storage offset is S
+  uint32_t m = 0;
+#define LBM_LA(Q) if (SDir<Q, SW>::x == S) m |= 1u << Q;
+  LBM_LA(1) LBM_LA(2) LBM_LA(3) LBM_LA(4) LBM_LA(5) LBM_LA(6) LBM_LA(7) LBM_LA(8) LBM_LA(9)
+  LBM_LA(10) LBM_LA(11) LBM_LA(12) LBM_LA(13) LBM_LA(14) LBM_LA(15) LBM_LA(16) LBM_LA(17) LBM_LA(18)
+#undef LBM_LA
+  return m;
+}
+__device__ __forceinline__ uint32_t u_from_prev(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t u_from_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, false);
+}
+// called with the whole wave active (the DPP shifts read every lane); g: this lane's groups
+template <int Q, bool SW>
+__device__ __forceinline__ void bb_group_one(float* __restrict__ dst, int64_t c, uint32_t g, const f4* v, int pitch,
+                                             int64_t plane) {
+  if constexpr (Q > 0) {
+    const bool mine = (g >> Q) & 1u;
+    if (__any(mine)) {  // wave-uniform
+      constexpr int s = SDir<Q, SW>::x;
+      const f4 o = v[Dir<Q>::opp];
+      f4 w;
+      if constexpr (s == 0) w = o;
+      else if constexpr (s == 1) w = f4{o.y, o.z, o.w, lane_from_next(o.x)};
+      else w = f4{lane_from_prev(o.w), o.x, o.y, o.z};
+      if (mine) *reinterpret_cast<f4*>(dst + aidx(c - row_off<Q, SW>(pitch, plane), Q)) = w;
+    }
+  }
+}
+template <bool SW, int... Qs>
+__device__ __forceinline__ void bb_group_all(float* __restrict__ dst, int64_t c, uint32_t g, const f4* v, int pitch,
+                                             int64_t plane, std::integer_sequence<int, Qs...>) {
+  (bb_group_one<Qs, SW>(dst, c, g, v, pitch, plane), ...);
+}
 
 // moments (ldc.cu:316-322): sequential fp32 sum; signed sums in the reference order
 template <int J>
@@ -469,6 +512,19 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     relax_cell<1, false>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
     relax_cell<2, false>(v, a.tau, a.tau_rcp, r2, x2, y2, z2, AllQ{});
     relax_cell<3, false>(v, a.tau, a.tau_rcp, r3, x3, y3, z3, AllQ{});
+  }
+  if (__any(t4 & kWall4)) {  // wave-uniform: whole-group bounce-back stores (bb_group_one)
+    const uint32_t b0 = (store & 1u) ? m0 : 0u, b1 = (store & 2u) ? m1 : 0u, b2 = (store & 4u) ? m2 : 0u,
+                   b3 = (store & 8u) ? m3 : 0u;
+    const uint32_t nb0 = take_hi ? 0u : u_from_next(b0), pb3 = take_lo ? 0u : u_from_prev(b3);
+    const uint32_t g0 = b0 & b1 & b2 & b3 & links_along<SW, 0>();
+    const uint32_t gp = b1 & b2 & b3 & nb0 & links_along<SW, 1>();   // G takes the next lane's cell 0
+    const uint32_t gm = pb3 & b0 & b1 & b2 & links_along<SW, -1>();  // G takes the previous lane's cell 3
+    const uint32_t gpp = take_lo ? 0u : u_from_prev(gp);  // the previous lane's G holds my cell 0's wall
+    const uint32_t gmn = take_hi ? 0u : u_from_next(gm);  // the next lane's G holds my cell 3's wall
+    bb_group_all<SW>(a.dst, c, g0 | gp | gm, v, a.pitch, a.plane, AllQ{});
+    const uint32_t g = g0 | gp | gm;
+    m0 &= ~(g0 | gm | gpp); m1 &= ~g; m2 &= ~g; m3 &= ~(g0 | gp | gmn);
   }
   if (t4 & kWall4) {  // rare, divergent: lanes holding wall-adjacent cells
     if (store & 1u) bb_store_cell<0, SW>(a.dst, c, m0, v, a.pitch, a.plane);
