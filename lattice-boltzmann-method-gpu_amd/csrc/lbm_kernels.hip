@@ -453,7 +453,15 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   // so this dependent load hides behind the arithmetic)
   constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
   uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-  if (t4 & kWall4) {
+  if constexpr (GROUPS) {
+    // compact lists are wall-heavy: the lane's four masks go out beside the type bytes (one
+    // 16-B load, no dependent round trip)
+    const uint4 lk = *reinterpret_cast<const uint4*>(a.links + (need ? c : 0));
+    m0 = (t4 & (kWallAdj << 0)) ? lk.x : 0u;
+    m1 = (t4 & (kWallAdj << 8)) ? lk.y : 0u;
+    m2 = (t4 & (kWallAdj << 16)) ? lk.z : 0u;
+    m3 = (t4 & (kWallAdj << 24)) ? lk.w : 0u;
+  } else if (t4 & kWall4) {
     if (t4 & (kWallAdj << 0)) m0 = a.links[c + 0];
     if (t4 & (kWallAdj << 8)) m1 = a.links[c + 1];
     if (t4 & (kWallAdj << 16)) m2 = a.links[c + 2];
