@@ -866,8 +866,8 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
   if (threadIdx.x == 0) a.partial[slot] = s;
 }
 
-// 4 cells per lane (big lattices): two waves per SIMD (210-252 VGPRs); MASK: the range has
-// lane masks (sparse chunk lists)
+// 4 cells per lane (big lattices): two waves per SIMD (210-253 VGPRs; one exact-division-only
+// instance runs one); MASK: the range has lane masks (sparse chunk lists)
 template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
   step_body<FAST, false, SW, MASK, STRIDE, GROUPS>(a);
