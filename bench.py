@@ -66,45 +66,36 @@ def cpu_baseline(n: int = 512, steps: int = 1):
 
 
 def pmc_traffic(workload: str):
-    """HBM bytes per k_step launch measured by rocprofv3 PMC passes
-    (tools/gpu_profile.sh + tools/pmc_traffic.py write profiles/pmc_traffic.json)."""
+    """HBM bytes per k_step launch measured by rocprofv3 PMC passes (tools/gpu_profile.sh +
+    tools/pmc_traffic.py, tools/pmc_lattices.sh + .py write profiles/pmc_traffic.json) -- only
+    when recorded on the kernels this run uses (lbm_amd.kernel_fingerprint()); an entry from
+    other kernels comes back as {"stale": tag} and is not reported as this run's traffic."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(p)).get(workload)
+        e = json.load(open(p)).get(workload)
     except (OSError, ValueError):
         return None
+    if e and e.get("kernel_src") != lbm_amd.kernel_fingerprint():
+        return {"stale": e.get("tag")}
+    return e
 
 
-def small_case_mlups(n: int, steps: int, dev: int):
-    lat = cases.ldc_device(n, n, n, device=dev)
-    lat.step(20, history=False)
-    lat.sync()
-    t = time.perf_counter()
-    lat.step(steps, history=False)
-    lat.sync()
-    dt = time.perf_counter() - t
-    lat.close()
-    return round(n ** 3 * steps / dt / 1e6, 1)
+def ldc_line(n: int, steps: int, dev: int, name: str):
+    """LDC n^3 (device-generated cavity) through timed_mlups: wall-clock MLUPS plus k_step's
+    own roofline and, when profiled on these kernels, its measured HBM traffic."""
+    return timed_mlups(cases.ldc_device(n, n, n, device=dev), {"mlups": n ** 3}, steps, name=name)
 
 
 def c5_one_gpu(dev: int, steps: int = 10):
     """The C5 lattice (LDC 512 x 512 x 4096, 1.07 G cells, ~187 GB) as ONE domain on one GPU:
-    what the 8-GPU configuration's total work costs a single MI355X."""
+    what the 8-GPU configuration's total work costs a single MI355X (timed_mlups: k_step's
+    roofline from HIP events, traffic when profiled)."""
     t = time.perf_counter()
     lat = cases.ldc_device(512, 512, 4096, device=dev)
     setup = time.perf_counter() - t
-    lat.step(3, history=False)
-    lat.sync()
-    lat.profile(True)
-    t = time.perf_counter()
-    lat.step(steps, history=False)
-    lat.sync()
-    dt = time.perf_counter() - t
-    st = lat.stats()
-    lat.close()
-    return {"mlups": round(512 * 512 * 4096 * steps / dt / 1e6, 1), "steps": steps,
-            "avg_kernel_ms": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]), 3),
-            "setup_s": round(setup, 1)}
+    out = timed_mlups(lat, {"mlups": 512 * 512 * 4096}, steps, warm=3, name="ldc_512x512x4096 (C5 lattice)")
+    out["setup_s"] = round(setup, 1)
+    return out
 
 
 def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
@@ -114,6 +105,7 @@ def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
     tools/pmc_lattices.sh) when present."""
     lay = lat.layout()
     shape = lat.launch_shape()
+    store = lat.storage()
     algo = lat.counts()["algo_bytes_per_step"]
     lat.step(warm, history=False)
     lat.sync()
@@ -131,13 +123,17 @@ def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
     out["cells_per_lane"] = shape["cells_per_lane"]
     out["grid_stride"] = shape["grid_stride"]
     out["lane_fill"] = shape["lane_fill"]
+    out["storage"] = {"compact_rows": store["compact"], "cell_slots": store["cells"],
+                      "population_bytes": store["bytes"]}
     kms = st["step_kernel_ms"] / max(1, st["step_kernel_launches"])
     if kms > 0:
         gbs = algo / (kms * 1e-3) / 1e9
         rl = {"avg_kernel_us": round(kms * 1e3, 2), "algo_bytes_per_launch": int(algo),
               "achieved": round(gbs, 1), "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None}
         pmc = pmc_traffic(name) if name else None
-        if pmc:
+        if pmc and "stale" in pmc:
+            rl["traffic_stale"] = f"profiles/pmc_traffic.json ({pmc['stale']}) was measured on other kernels"
+        elif pmc:
             rl["traffic"] = pmc["bytes_per_launch"]
             rl["traffic_over_algo"] = pmc.get("traffic_over_algo")
             rl["traffic_source"] = f"profiles/pmc_traffic.json ({pmc.get('tag')}, tools/pmc_lattices.sh)"
@@ -388,6 +384,9 @@ def main():
     achieved = algo_bytes / (main_step_ms * 1e-3) / 1e9
     workload = f"ldc_{n}x{n}x{n}_per_gpu"
     pmc = pmc_traffic(workload)
+    stale = pmc.get("stale") if pmc else None
+    if stale:
+        pmc = None
     line = {
         "metric": "MLUPS (million lattice updates/sec) + achieved HBM GB/s vs roofline",
         "value": round(mlups, 1),
@@ -420,7 +419,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc.get("bytes_per_launch") if pmc else None,
             "traffic_source": (f"profiles/pmc_traffic.json ({pmc.get('tag')}: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
-                               f"per launch, 512^3 N=1)") if pmc else None,
+                               f"per launch, 512^3 N=1, same kernel fingerprint)") if pmc else
+                              (f"stale: profiles/pmc_traffic.json ({stale}) was measured on other kernels" if stale
+                               else None),
             "algo_bytes_per_launch": algo_bytes,
             "avg_kernel_ms": round(main_avg_ms, 4),
             "kernel_ms_per_step": round(main_step_ms, 4),
@@ -439,14 +440,15 @@ def main():
         "buffer_placement": placement,
         "launch_shape": launch_shape,
         "residual_last": state["residual"],
+        "kernel_src": lbm_amd.kernel_fingerprint(),
     }
     if world > 1:
         line["multi_gpu"] = multi_gpu_block(every)
     if world == 1 and not args.no_secondary:
-        line["secondary"] = {"ldc64_mlups (published config)": small_case_mlups(64, 2000, local),
-                             "ldc256_mlups (config C2)": small_case_mlups(256, 200, local),
+        line["secondary"] = {"ldc_64^3 (published config)": ldc_line(64, 2000, local, "ldc_64^3"),
+                             "ldc_256^3 (C2)": ldc_line(256, 200, local, "ldc_256^3 (C2)"),
                              f"ldc{n}_random_velocity_start": perturbed_mlups(n, 50, local),
-                             "ldc512x512x4096_one_gpu (C5 lattice, single domain)": c5_one_gpu(local),
+                             "ldc_512x512x4096 (C5 lattice, single domain)": c5_one_gpu(local),
                              **config_lines(local)}
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

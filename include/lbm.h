@@ -171,9 +171,8 @@ typedef enum {
                                    when the chunks' lanes are under 3/4 busy, else one chunk per
                                    wave; 1 one chunk (or list slice) per wave; B = 2..8 the loop
                                    with at most B blocks per CU (sparse lists only) */
-  LBM_TUNE_INJECT_RCCL_FAULT = 7, /* test hook: 1 = the next wait of an RCCL context (lbm_sync, a
-                                   synchronising lbm_step, a read-out) sees a failed peer; the knob
-                                   resets itself.  Exercises the abort path below. */
+  LBM_TUNE_INJECT_RCCL_FAULT = 7, /* reserved (was a process-wide fault-injection hook; now per
+                                   context: lbm_debug_fail_next_wait); only 0 is accepted */
   LBM_TUNE_GROUPS = 8,          /* sparse chunk lists: 0 (default) compact lists of the active 4-cell
                                    groups when the chunks' lanes (one cell per lane: cells) are under
                                    3/4 busy, 1 never, 2 on every sparse list.  With CELLS_PER_LANE 0
@@ -182,7 +181,13 @@ typedef enum {
   LBM_TUNE_GROUP_SEGMENT = 9,   /* group lists: 1..64 groups per segment (default 8: one 128-B line);
                                    a segment with an active group enters the list whole, its idle
                                    groups load nothing */
-  LBM_TUNE_COUNT = 10
+  LBM_TUNE_COMPACT = 10,        /* storage of single-domain lattices whose step takes group lists
+                                   (vessel trees): 0 (default) compact rows -- every storage row keeps
+                                   only the span of its stored cells, packed in storage order (the
+                                   reference's index_transform, Poiseulle.cu:257-271, per row); 1 the
+                                   dense box; 2 compact rows whenever the range takes group lists
+                                   (LBM_TUNE_GROUPS 2 included) */
+  LBM_TUNE_COUNT = 11
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 
@@ -294,13 +299,19 @@ int lbm_get_layout(lbm_ctx* ctx, int* row_axis, int* pitch, int* x_align, int64_
  * for benchmarks and tests): cells_per_lane 1 or 4, main_blocks = its chunk workgroups,
  * grid_stride 1 when those loop over their XCD's chunks (LBM_TUNE_GRID_STRIDE), 2 when its
  * waves take compact lists of active 4-cell groups (LBM_TUNE_GROUPS; 64 groups per wave with
- * four cells per lane, 16 with one); lane_fill = mean share of chunk lanes (one cell per lane:
- * of the chunks' cells; with groups: of a listed group's cells) with a cell to update.
+ * four cells per lane, 16 with one), 3 when one-cell waves take consecutive cells of compact
+ * rows (LBM_TUNE_COMPACT; no list); lane_fill = mean share of chunk lanes (one cell per lane:
+ * of the chunks' cells; with groups: of a listed group's cells; compact rows without a list:
+ * of the waves' cells) with a cell to update.
  * Nullable outputs. */
 int lbm_get_launch_shape(lbm_ctx* ctx, int* cells_per_lane, int* main_blocks, int* grid_stride, double* lane_fill);
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (each stores its NEE
  * neighbours' values, producer side). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
+/* Population storage (not a reference interface): compact = 1 when the lattice is stored in
+ * compact rows (LBM_TUNE_COMPACT), cells = cell slots per population buffer (the padded box, or
+ * the compact rows' spans), bytes = both population buffers' device bytes.  Nullable outputs. */
+int lbm_get_storage(lbm_ctx* ctx, int* compact, int64_t* cells, int64_t* bytes);
 
 /* Measurement helper (not a reference interface): the HBM rate a plain streaming copy
  * reaches on this device, for context next to k_step's roofline fraction.  Copies `bytes`
@@ -328,6 +339,10 @@ int lbm_attach_rccl(lbm_ctx* ctx, const uint8_t id[128], int rank, int nranks);
  * lbm_step, lbm_sync, every read-out, lbm_checkpoint_save and lbm_comm_info return
  * LBM_ERR_RCCL (the slab's ghost planes and residual are stale); destroy the context. */
 int lbm_comm_info(lbm_ctx* ctx, int* rank, int* nranks);
+/* Test hook (not a reference interface): the next wait of THIS context (lbm_sync, a
+ * synchronising lbm_step, a read-out) sees a failed peer, which exercises the abort path above.
+ * Only contexts with an RCCL communicator wait that way (LBM_ERR_STATE otherwise). */
+int lbm_debug_fail_next_wait(lbm_ctx* ctx);
 
 /* Single-device loopback decomposition (test and debug path): n contexts, each a z-slab of
  * one lattice on the same device, stepped together with device-to-device halo copies. */

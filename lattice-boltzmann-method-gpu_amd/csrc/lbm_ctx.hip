@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -61,11 +61,14 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   uint32_t* cell_nl = nullptr;  // their NEE-link masks
   float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
+  bool nee_chunks = false;  // 4-cell ranges: chunk waves also store the NEE-adjacent cells (MainArgs)
   int* groups = nullptr;  // sparse ranges: compact list of active 4-cell groups (both paths)
   int64_t ngroups = 0;
   int* group_bc = nullptr;         // one-cell group lists: per entry, its NEE records' index or -1
   float4* group_rec = nullptr;     // kNeeSlots records per cell of the groups with NEE-adjacent cells
   double group_fill = 0.0;  // mean share of a listed group's cells the wave updates
+  int* group_row = nullptr;  // compact rows: the storage row of every group-list entry
+  int* cell_row = nullptr;   // compact rows: the storage row of every NEE-block cell
   unsigned long long* lane_masks = nullptr;  // 4-cell path, sparse ranges: lanes a chunk wave loads
   double* part = nullptr; // one |u| partial per block (NEE blocks, then chunk blocks)
   int npart = 0;
@@ -80,7 +83,8 @@ struct lbm_ctx {
   lbm_desc d{};
   Layout L{};
   hipStream_t s_comp = nullptr, s_comm = nullptr;
-  hipEvent_t ev_edge = nullptr, ev_halo = nullptr, ev_sum = nullptr, ev_fin = nullptr;
+  hipEvent_t ev_edge = nullptr, ev_halo = nullptr, ev_mid = nullptr, ev_fin = nullptr;
+  hipEvent_t ev_sum[2] = {nullptr, nullptr};  // slab step: the reduction of step h read partials[h & 1]
   float* alloc[2] = {nullptr, nullptr};  // hipMalloc'd population buffers
   std::vector<double> cand_gbs;           // buffer_placement: candidates' sweep-write rates (GB/s)
   int chosen[2] = {0, 1};                 // the two candidates kept
@@ -98,6 +102,7 @@ struct lbm_ctx {
   int red_n = 0;               // whole.npart + 8 (the leading reduction group)
   bool fuse_red = false;
   int npart_slab = 0;
+  double* slab_part = nullptr;  // RCCL slab step: 2 x npart_slab partials by step parity
   double* scratch = nullptr;
   ConvState* conv = nullptr;
   float* hist = nullptr;
@@ -137,6 +142,7 @@ struct lbm_ctx {
   // and the residual are stale from then on, so every later step, wait and read-out fails with
   // LBM_ERR_RCCL instead of silently running the slab as a single domain
   bool comm_failed = false;
+  bool inject_fault = false;  // lbm_debug_fail_next_wait: the next wait sees a failed peer
   // residual summation order (lbm_set_residual_order): LBM_SUM_FP64, or the reference-order
   // fp32 CUB tree over n_ref terms (ref_idx: reference storage slot per fluid cell, -1 else)
   int sum_mode = LBM_SUM_FP64;
@@ -145,6 +151,21 @@ struct lbm_ctx {
   float* terms = nullptr;
   float* cub_part = nullptr;
   int64_t n_ref = 0;
+  // Compact rows (LBM_TUNE_COMPACT; single-domain lattices whose step takes group lists): buf[]
+  // hold only the spans of stored cells of every storage row, packed in storage order, and the
+  // kernels read compact copies of the per-cell arrays (ctype ... cuz, indexed like buf).  The
+  // dense arrays above stay for set-up and read-out, which run on a dense staging copy of a
+  // population buffer (stage_dense / from_dense).
+  bool compact = false;
+  int64_t ncell_c = 0, nchunk_c = 0, guard_c = 0;  // compact cell slots (whole chunks), guard chunks
+  int* cmap = nullptr;     // device: the dense cell of every compact cell, -1 for none
+  int4* rowrec = nullptr;  // device: per storage row the nine neighbour-row offsets (MainArgs::rowrec)
+  int4* grouprec = nullptr;  // device, one-cell compact ranges: rowrec of every compact group's row
+  uint8_t* ctype = nullptr;
+  uint32_t *clinks = nullptr, *cnlinks = nullptr;
+  float *crho = nullptr, *cux = nullptr, *cuy = nullptr, *cuz = nullptr;
+  // slots per population buffer past the leading guard (the part checkpoints hold)
+  int64_t pop_floats() const { return (compact ? nchunk_c : L.nchunk) * kQ * kChunk; }
   std::string err;
 };
 
@@ -308,8 +329,15 @@ struct FusedRed {
 void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
   a.src = c->buf[srcbuf];
   a.dst = c->buf[srcbuf ^ 1];
-  a.type = c->type; a.links = c->links; a.nlinks = c->nlinks;
-  a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
+  if (c->compact) {
+    a.type = c->ctype; a.links = c->clinks; a.nlinks = c->cnlinks;
+    a.rho = c->crho; a.ux = c->cux; a.uy = c->cuy; a.uz = c->cuz;
+    a.rowrec = c->rowrec;
+    a.grouprec = c->grouprec;
+  } else {
+    a.type = c->type; a.links = c->links; a.nlinks = c->nlinks;
+    a.rho = c->rho; a.ux = c->ux; a.uy = c->uy; a.uz = c->uz;
+  }
   a.pitch = c->L.pitch; a.plane = c->L.plane;
   a.tau = c->tau;
   a.tau_rcp = 1.0f / c->tau;
@@ -322,10 +350,11 @@ void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
 }
 
 // one step of a range from buffer srcbuf into srcbuf ^ 1
-int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* fr = nullptr, int range_kind = -1) {
+int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* fr = nullptr, int range_kind = -1,
+              double* part = nullptr) {
   MainArgs a{};
   fill_main_args(c, a, srcbuf);
-  a.partial = r.part;
+  a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
@@ -333,11 +362,14 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.ngroups = r.ngroups;
   a.group_bc = r.group_bc;
   a.group_rec = r.group_rec;
+  a.group_row = r.group_row;
+  a.cell_row = r.cell_row;
   a.c_lo = r.c_lo; a.c_hi = r.c_hi; a.c_lo2 = r.c_lo2; a.c_hi2 = r.c_hi2;
   a.fast_div = (c->fast_div && !r.quarter) ? 1 : 0;
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
   a.cells = r.cells; a.cell_nl = r.cell_nl; a.nee_bc = r.nee_bc; a.n_nee = r.n_nee;
   a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
+  a.nee_chunks = r.nee_chunks ? 1 : 0;
   if (fr) {
     a.partial = fr->part;
     a.red_blocks = 8;
@@ -357,9 +389,37 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   return LBM_OK;
 }
 
-// work lists of the cells [lo, hi) u [lo2, hi2) from the host copy of the type bytes
-int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t, int64_t lo2 = 0,
-                int64_t hi2 = 0) {
+// device scratch freed on every exit path of build_range
+struct DevScratch {
+  void* p = nullptr;
+  ~DevScratch() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// build_range over compact rows: the cells are compact ids (the lists index the compact arrays);
+// dense_of translates them for the gathers of boundary records from the dense arrays, row_of
+// gives every compact 4-cell group's storage row; the dense range's one-cell choice is kept and
+// the waves always take group lists
+struct CompactView {
+  const std::vector<int>* dense_of;
+  const std::vector<int>* row_of;
+  bool quarter;
+};
+
+// upload a host vector (n >= 1) into a fresh device array
+template <class T>
+int upload(lbm_ctx* c, T** dev, const std::vector<T>& h) {
+  HIPCK(c, hipMalloc(dev, sizeof(T) * std::max<size_t>(1, h.size())));
+  if (!h.empty()) HIPCK(c, hipMemcpy(*dev, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  return LBM_OK;
+}
+
+// work lists of the cells [lo, hi) u [lo2, hi2) from host copies of the type bytes and of the
+// NEE-link masks k_flag_fluid wrote (the masks the kernels read, so the gathered boundary
+// records are indexed exactly as the kernels index them)
+int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t,
+                const std::vector<uint32_t>& nlk, int64_t lo2 = 0, int64_t hi2 = 0, const CompactView* cv = nullptr) {
   if (lo2 < hi) lo2 = hi2 = 0;  // overlapping second interval (single-plane slab): drop it
   r.c_lo = lo;
   r.c_hi = hi;
@@ -367,6 +427,25 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   r.c_hi2 = hi2;
   std::vector<int> chunks, cells;
   auto in = [&](int64_t k) { return (k >= lo && k < hi) || (k >= lo2 && k < hi2); };
+  // Chunk waves also take the NEE-adjacent cells (nee_chunks) when those mostly share their
+  // 4-cell group with other fluid cells -- the pipe's rows along y, vessel trees: each such
+  // group would otherwise store cell by cell, and every wave holding one would issue both store
+  // paths (C3 -0.6%, C4 x4 -1.6% in interleaved A/B, profiles/r04_nee_chunks_ab.log).  Groups
+  // made only of NEE-adjacent cells (the cavity's lid rows) stay with the NEE blocks: there the
+  // chunk waves would load and store whole extra rows (LDC 512^3 +1%).
+  {
+    int64_t mixed = 0, pure = 0;
+    for (int64_t g = (lo & ~int64_t(3)); g < std::max(hi, hi2); g += 4) {
+      int nee = 0, other = 0;
+      for (int64_t k = g; k < g + 4; ++k) {
+        if (!in(k) || (t[k] & kClassMask) != kFluid) continue;
+        if (t[k] & kNeeAdj) ++nee;
+        else ++other;
+      }
+      if (nee) ++(other ? mixed : pure);
+    }
+    r.nee_chunks = mixed > pure;
+  }
   auto scan = [&](int64_t a, int64_t b) {
     for (int64_t ch = a / kChunk; ch * kChunk < b; ++ch) {
       if (!chunks.empty() && chunks.back() >= (int)ch) continue;  // chunk shared by both intervals
@@ -402,14 +481,16 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     // one cell per lane; the upsampled bifurcation (15k) keeps four cells per lane (+2% the
     // other way; profiles/r03_groups1_ab.log).
     const int gm = g_tune[LBM_TUNE_GROUPS];
-    if (!cpl && !r.quarter && r.chunk0 < 0 && gm != 1) {
+    if (cv) {
+      r.quarter = group1 = cv->quarter;
+    } else if (!cpl && !r.quarter && r.chunk0 < 0 && gm != 1) {
       int64_t active = 0;
       for (int ch : chunks)
         for (int l = 0; l < 64; ++l) {
           bool any = false;
           for (int k = 0; k < 4; ++k) {
             const int64_t cell = (int64_t)ch * kChunk + 4 * l + k;
-            any |= in(cell) && (t[cell] & kClassMask) == kFluid && !(t[cell] & kNeeAdj);
+            any |= in(cell) && (t[cell] & kClassMask) == kFluid && (r.nee_chunks || !(t[cell] & kNeeAdj));
           }
           active += any;
         }
@@ -417,30 +498,15 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       if ((gm == 2 || fill4 < 0.75) && (active + 63) / 64 <= kQuarterMaxChunks) r.quarter = group1 = true;
     }
   }
-  // 4-cell ranges: the NEE-adjacent cells go to NEE blocks, one per thread.  In a chunk wave
-  // each would add two dependent load rounds (its NEE-link mask, then its neighbours' boundary
-  // data) to the whole wave -- on the pipe with rows along y, to every wave.  One-cell waves
-  // load the link mask with the pulls and keep them (the boundary data arrives under the
-  // arithmetic).
+  // 4-cell ranges: the NEE values of the NEE-adjacent cells go to NEE blocks, one cell per
+  // thread.  In a chunk wave each would add two dependent load rounds (its NEE-link mask, then
+  // its neighbours' boundary data) to the whole wave -- on the pipe with rows along y, to every
+  // wave.  One-cell waves load the link mask with the pulls and keep them (the boundary data
+  // arrives under the arithmetic).
   double contig = 1.0;
   if (r.quarter) cells.clear();
   // the NEE-link mask of k_flag_fluid: q crosses the NEE neighbour's face (e_q . n == 1)
-  int64_t off[kQ];
-  for (int q = 0; q < kQ; ++q) {
-    const int s0 = c->L.swap ? kEy[q] : kEx[q], s1 = c->L.swap ? kEx[q] : kEy[q];
-    off[q] = s0 + (int64_t)s1 * c->L.pitch + (int64_t)kEz[q] * c->L.plane;
-  }
-  auto nl_of = [&](int64_t cell) {
-    uint32_t m = 0;
-    for (int q = 1; q < kQ; ++q) {
-      const int64_t nb = cell - off[q];
-      if (nb < 0 || nb >= (int64_t)t.size() || (t[nb] & kClassMask) != kNee) continue;
-      const int fb = (kEx[q] == 1 ? 1 : 0) | (kEx[q] == -1 ? 2 : 0) | (kEy[q] == 1 ? 4 : 0) |
-                     (kEy[q] == -1 ? 8 : 0) | (kEz[q] == 1 ? 16 : 0) | (kEz[q] == -1 ? 32 : 0);
-      if ((fb >> nee_face(t[nb])) & 1) m |= 1u << q;
-    }
-    return m;
-  };
+  auto nl_of = [&](int64_t cell) { return nlk[cell]; };
   r.n_nee = (int)cells.size();
   if (r.n_nee) {
     std::vector<uint32_t> nl(cells.size());
@@ -464,13 +530,29 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMalloc(&r.cell_nl, sizeof(uint32_t) * r.n_nee));
     HIPCK(c, hipMemcpy(r.cell_nl, snl.data(), sizeof(uint32_t) * r.n_nee, hipMemcpyHostToDevice));
     // the boundary cells' data is written by classification and never changes afterwards
+    // (gathered from the dense arrays: compact cells are translated first)
     HIPCK(c, hipMalloc(&r.nee_bc, sizeof(float4) * kNeeSlots * r.n_nee));
-    HIPCK(c, launch_nee_gather(r.cells, r.cell_nl, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.n_nee, c->L.pitch,
+    DevScratch dense_ids;
+    const int* gather_ids = r.cells;
+    if (cv) {
+      std::vector<int> dsc(sc.size()), rows(sc.size());
+      for (size_t i = 0; i < sc.size(); ++i) {
+        dsc[i] = (*cv->dense_of)[sc[i]];
+        rows[i] = (*cv->row_of)[sc[i] >> 2];
+      }
+      int* p = nullptr;
+      RCK(upload(c, &p, dsc));
+      dense_ids.p = p;
+      gather_ids = p;
+      RCK(upload(c, &r.cell_row, rows));
+    }
+    HIPCK(c, launch_nee_gather(gather_ids, r.cell_nl, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.n_nee, c->L.pitch,
                                c->L.plane, c->L.swap, c->s_comp));
     HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   // Lane masks for the 4-cell path: bit l of a chunk's mask is set when lane l (cells 4l ..
-  // 4l+3) holds a cell the chunk wave updates (fluid, in range, not NEE-adjacent) or neighbours
+  // 4l+3) holds a cell the chunk wave updates (fluid, in range, not NEE-adjacent unless
+  // nee_chunks) or neighbours
   // such a lane (the DPP x-shift reads the next lanes' slices).  Lanes outside it load nothing:
   // on a vessel tree most chunks are partly empty (the upsampled bifurcation keeps 51% of its
   // active chunks' cells).  Only for sparse chunk lists, whose waves load their chunk id
@@ -479,9 +561,9 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // lines); their fill -- cells to update over the active chunks' cells -- picks the group list.
   auto updated = [&](int64_t cell) {
     const uint8_t v = t[cell];
-    return in(cell) && (v & kClassMask) == kFluid && (r.quarter || !(v & kNeeAdj));
+    return in(cell) && (v & kClassMask) == kFluid && (r.quarter || r.nee_chunks || !(v & kNeeAdj));
   };
-  if (r.nchunks && r.chunk0 < 0) {
+  if (r.nchunks && r.chunk0 < 0 && !cv) {
     std::vector<unsigned long long> lm(chunks.size());
     bool partial = false;
     int64_t busy = 0, cells_busy = 0;
@@ -515,11 +597,48 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // keep their loads and stores
   // contiguous, and a group whose list neighbour is not its row neighbour loads its x-edge
   // cells itself (pull_issue).
-  {
+  if (cv && r.quarter) {
+    // compact rows, one cell per lane: no list -- wave w takes the compact cells from
+    // (lo & ~63) + 64 w (process_compact_cell1); the boundary records of the NEE-adjacent cells
+    // by compact group (group_bc), gathered from the dense arrays
+    const int64_t base = lo & ~int64_t(63), waves = (hi - base + 63) / 64;
+    r.main_blocks = waves ? (int)std::max<int64_t>(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
+    int64_t fl = 0;
+    for (int64_t k = lo; k < hi; ++k) fl += (t[k] & kClassMask) == kFluid;
+    r.group_fill = hi > base ? (double)fl / (double)(64 * waves) : 1.0;
+    if (!c->bc_uniform) {
+      std::vector<int> gbc((size_t)(t.size() / 4), -1), gcells;
+      std::vector<uint32_t> gnl;
+      auto nee_adj = [&](int64_t k) { return in(k) && (t[k] & kClassMask) == kFluid && (t[k] & kNeeAdj); };
+      int nrec = 0;
+      for (int64_t g = base / 4; g < (hi + 3) / 4; ++g) {
+        if (!(nee_adj(4 * g) || nee_adj(4 * g + 1) || nee_adj(4 * g + 2) || nee_adj(4 * g + 3))) continue;
+        gbc[g] = nrec++;
+        for (int64_t j = 4 * g; j < 4 * g + 4; ++j) {
+          gcells.push_back(std::max(0, (*cv->dense_of)[j]));
+          gnl.push_back(nee_adj(j) ? nl_of(j) : 0u);
+        }
+      }
+      if (nrec) {
+        DevScratch dc, dn;
+        RCK(upload(c, &r.group_bc, gbc));
+        HIPCK(c, hipMalloc(&r.group_rec, sizeof(float4) * kNeeSlots * gcells.size()));
+        int* pc = nullptr;
+        uint32_t* pn = nullptr;
+        RCK(upload(c, &pc, gcells));
+        dc.p = pc;
+        RCK(upload(c, &pn, gnl));
+        dn.p = pn;
+        HIPCK(c, launch_nee_gather(pc, pn, c->rho, c->ux, c->uy, c->uz, r.group_rec, (int)gcells.size(), c->L.pitch,
+                                   c->L.plane, c->L.swap, c->s_comp));
+        HIPCK(c, hipStreamSynchronize(c->s_comp));
+      }
+    }
+  } else {
     const int gm = g_tune[LBM_TUNE_GROUPS];
     const bool sparse = r.quarter ? r.lane_fill < kGroupFill1 : r.lane_masks && r.lane_fill < 0.75;
-    const bool want = gm == 2 || (gm == 0 && (sparse || group1));
-    if (r.nchunks && r.chunk0 < 0 && want) {
+    const bool want = cv || gm == 2 || (gm == 0 && (sparse || group1));
+    if (r.nchunks && (r.chunk0 < 0 || cv) && want) {
       // segments of seg groups (LBM_TUNE_GROUP_SEGMENT, default 8 = one 128-B line of a chunk
       // slice): a segment with an active group enters the list whole, its idle groups marked
       // (bit 0) so their lanes load nothing.  Whole lines per wave load beat full lanes on the
@@ -546,6 +665,11 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       if (r.ngroups) {
         HIPCK(c, hipMalloc(&r.groups, sizeof(int) * gl.size()));
         HIPCK(c, hipMemcpy(r.groups, gl.data(), sizeof(int) * gl.size(), hipMemcpyHostToDevice));
+        if (cv) {
+          std::vector<int> rows(gl.size());
+          for (size_t i = 0; i < gl.size(); ++i) rows[i] = (*cv->row_of)[gl[i] >> 2];
+          RCK(upload(c, &r.group_row, rows));
+        }
       }
       // one-cell waves: the boundary records of the groups holding NEE-adjacent cells, gathered
       // once and indexed by list entry (process_group_cell1 loads them with the pulls)
@@ -560,25 +684,24 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
           if (!(nee_adj(g) || nee_adj(g + 1) || nee_adj(g + 2) || nee_adj(g + 3))) continue;
           gbc[i] = nrec++;
           for (int64_t j = g; j < g + 4; ++j) {
-            gcells.push_back((int)j);
+            // the records are gathered from the dense arrays: compact cells translated
+            gcells.push_back(cv ? std::max(0, (*cv->dense_of)[j]) : (int)j);
             gnl.push_back(nee_adj(j) ? nl_of(j) : 0u);
           }
         }
         if (nrec) {
-          int* dc = nullptr;
-          uint32_t* dn = nullptr;
+          DevScratch dc, dn;
           HIPCK(c, hipMalloc(&r.group_bc, sizeof(int) * gbc.size()));
           HIPCK(c, hipMemcpy(r.group_bc, gbc.data(), sizeof(int) * gbc.size(), hipMemcpyHostToDevice));
           HIPCK(c, hipMalloc(&r.group_rec, sizeof(float4) * kNeeSlots * gcells.size()));
-          HIPCK(c, hipMalloc(&dc, sizeof(int) * gcells.size()));
-          HIPCK(c, hipMalloc(&dn, sizeof(uint32_t) * gnl.size()));
-          HIPCK(c, hipMemcpy(dc, gcells.data(), sizeof(int) * gcells.size(), hipMemcpyHostToDevice));
-          HIPCK(c, hipMemcpy(dn, gnl.data(), sizeof(uint32_t) * gnl.size(), hipMemcpyHostToDevice));
-          HIPCK(c, launch_nee_gather(dc, dn, c->rho, c->ux, c->uy, c->uz, r.group_rec, (int)gcells.size(),
-                                     c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
+          HIPCK(c, hipMalloc(&dc.p, sizeof(int) * gcells.size()));
+          HIPCK(c, hipMalloc(&dn.p, sizeof(uint32_t) * gnl.size()));
+          HIPCK(c, hipMemcpy(dc.p, gcells.data(), sizeof(int) * gcells.size(), hipMemcpyHostToDevice));
+          HIPCK(c, hipMemcpy(dn.p, gnl.data(), sizeof(uint32_t) * gnl.size(), hipMemcpyHostToDevice));
+          HIPCK(c, launch_nee_gather(static_cast<const int*>(dc.p), static_cast<const uint32_t*>(dn.p), c->rho, c->ux,
+                                     c->uy, c->uz, r.group_rec, (int)gcells.size(), c->L.pitch, c->L.plane, c->L.swap,
+                                     c->s_comp));
           HIPCK(c, hipStreamSynchronize(c->s_comp));
-          (void)hipFree(dc);
-          (void)hipFree(dn);
         }
       }
       const int64_t waves = (r.ngroups + (r.quarter ? 15 : 63)) / (r.quarter ? 16 : 64);
@@ -616,9 +739,35 @@ void free_range(Range& r) {
   if (r.group_bc) (void)hipFree(r.group_bc);
   if (r.group_rec) (void)hipFree(r.group_rec);
   if (r.cells) (void)hipFree(r.cells);
+  if (r.group_row) (void)hipFree(r.group_row);
+  if (r.cell_row) (void)hipFree(r.cell_row);
   if (r.cell_nl) (void)hipFree(r.cell_nl);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
+}
+
+// Compact rows: a population buffer in the dense box layout for set-up and read-out (stage:
+// L.buf_floats() floats, the returned pointer past the guard), filled from compact buffer b
+// (to_dense) or copied into compact buffer b (from_dense)
+struct Stage {
+  float* alloc = nullptr;
+  ~Stage() {
+    if (alloc) (void)hipFree(alloc);
+  }
+};
+int stage_dense(lbm_ctx* c, Stage& st, float** base) {
+  HIPCK(c, hipMalloc(&st.alloc, sizeof(float) * c->L.buf_floats()));
+  HIPCK(c, hipMemsetAsync(st.alloc, 0, sizeof(float) * c->L.buf_floats(), c->s_comp));
+  *base = st.alloc + c->L.guard * kQ * kChunk;
+  return LBM_OK;
+}
+int to_dense(lbm_ctx* c, int b, float* dense) {
+  HIPCK(c, launch_pop_compact(dense, c->buf[b], c->cmap, c->ncell_c, 0, c->s_comp));
+  return LBM_OK;
+}
+int from_dense(lbm_ctx* c, const float* dense, int b) {
+  HIPCK(c, launch_pop_compact(c->buf[b], dense, c->cmap, c->ncell_c, 1, c->s_comp));
+  return LBM_OK;
 }
 
 int ensure_hist(lbm_ctx* c, int n) {
@@ -639,7 +788,14 @@ int reset_state(lbm_ctx* c) {
   cs.tol = host.tol;
   HIPCK(c, hipMemcpy(c->conv, &cs, sizeof(ConvState), hipMemcpyHostToDevice));
   if (c->bb_immediate) {  // LDC: walls already bounce back at step 0 (ldc.cu:75-202)
-    HIPCK(c, launch_bb_prime(c->buf[0], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
+    float* f = c->buf[0];
+    Stage st;
+    if (c->compact) {  // on a dense copy of buffer 0
+      RCK(stage_dense(c, st, &f));
+      RCK(to_dense(c, 0, f));
+    }
+    HIPCK(c, launch_bb_prime(f, c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap, c->s_comp));
+    if (c->compact) RCK(from_dense(c, f, 0));
     HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   c->steps_done = 0;
@@ -723,6 +879,147 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
   return e;
 }
 
+// Compact rows (LBM_TUNE_COMPACT), the reference's index_transform (Poiseulle.cu:257-271,
+// bifurcation.cu:241-252) done per storage row: a cell is stored when a fluid cell may read or
+// write it (fluid, wall, NEE, passive cells a fluid cell pulls) or the reference stores it
+// (code != 0: its ghost layer); every storage row r keeps the
+// span of 4-cell groups from its first to its last stored cell, the spans packed in storage
+// order, so cell (r, s0) lives at roff[r] + s0 with roff[r] = -xshift (mod 4) -- the groups and
+// the x-neighbours c +- 1 of the dense box, only the rows move.  On a vessel tree the waves'
+// loads then fill whole lines of the chunk slices instead of 128-B segments spread over
+// half-empty chunks of the box.  Builds the compact copies of the per-cell arrays, the row
+// records (MainArgs::rowrec) and the whole-domain range over compact cells; leaves c->compact
+// false when the lattice does not qualify (auto: compact rows must save 40% of the slots; their
+// buffers must stay under 2^31 floats for the kernels' 32-bit indices).
+int floordiv4(int x) { return x >= 0 ? x / 4 : -((-x + 3) / 4); }
+
+int build_compact(lbm_ctx* c, const std::vector<uint8_t>& t, const std::vector<uint32_t>& nlk) {
+  const Layout& L = c->L;
+  const int n0 = L.swap ? L.ny : L.nx, n1 = L.swap ? L.nx : L.ny;
+  const int64_t R = (int64_t)L.planes * n1, nt = (int64_t)t.size();
+  // the reference codes too: its stored cells (code != 0, ghosts included) keep their slots, so
+  // the initial state reads back like the dense box's (lbm_get_f)
+  std::vector<int8_t> codes((size_t)nt);
+  HIPCK(c, hipMemcpy(codes.data(), c->codes, nt, hipMemcpyDeviceToHost));
+  auto stored = [&](int64_t k) {
+    const uint8_t v = t[k];
+    return (v & kClassMask) != kPassive || (v & kPulled) || codes[k] != 0;
+  };
+  std::vector<int> roff(R, 0), glo(R, 0), ghi(R, -1), row_of;
+  std::vector<int64_t> gstart(R + 1, 0);
+  int64_t cum = 0;
+  for (int64_t r = 0; r < R; ++r) {
+    gstart[r] = cum;
+    const int64_t base = r * L.pitch - L.xshift;
+    int lo = -1, hi = -1;
+    for (int s = 0; s < n0; ++s) {
+      const int64_t k = base + s;
+      if (k < 0 || k >= nt || !stored(k)) continue;
+      if (lo < 0) lo = s;
+      hi = s;
+    }
+    if (lo < 0) continue;
+    glo[r] = floordiv4(lo - L.xshift);
+    ghi[r] = floordiv4(hi - L.xshift);
+    roff[r] = (int)(4 * (cum - glo[r]) - L.xshift);
+    for (int g = glo[r]; g <= ghi[r]; ++g) row_of.push_back((int)r);
+    cum += ghi[r] - glo[r] + 1;
+  }
+  gstart[R] = cum;
+  const int64_t ncell = (4 * cum + kChunk - 1) / kChunk * kChunk, nchunk = ncell / kChunk;
+  const int64_t guard = (n0 + 16 + kChunk - 1) / kChunk + 1;  // |offsets| of any lane's address
+  if (cum == 0 || (nchunk + 2 * guard) * kQ * kChunk >= (int64_t(1) << 31)) return LBM_OK;
+  if (g_tune[LBM_TUNE_COMPACT] == 0 && (double)ncell > 0.6 * (double)L.ncell) return LBM_OK;
+  row_of.resize(ncell / 4, row_of.back());  // the padding groups of the last chunk: the last row
+  std::vector<int> cmap(ncell, -1);
+  for (int64_t r = 0; r < R; ++r) {
+    if (ghi[r] < glo[r]) continue;
+    const int64_t base = r * L.pitch - L.xshift;
+    for (int s = 4 * glo[r] + L.xshift; s < 4 * ghi[r] + L.xshift + 4; ++s)
+      if (s >= 0 && s < n0 && base + s >= 0 && base + s < nt) cmap[roff[r] + s] = (int)(base + s);
+  }
+  std::vector<int> rec(R * 12, 0);
+  for (int64_t r = 0; r < R; ++r)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dz = -1; dz <= 1; ++dz) {
+        const int64_t rr = r + dy + (int64_t)dz * n1;
+        rec[r * 12 + (dy + 1) * 3 + dz + 1] = (rr >= 0 && rr < R) ? roff[rr] : 0;
+      }
+  // Every fluid cell's 18 neighbours, addressed the kernels' way (row record + position - e_x),
+  // must be exactly the compact slots of its dense neighbours: checked here, on the host, for
+  // every fluid cell, so a wrong row table fails lbm_create instead of reading stray slots
+  {
+    int64_t off[kQ];
+    for (int q = 0; q < kQ; ++q) {
+      const int s0 = L.swap ? kEy[q] : kEx[q], s1 = L.swap ? kEx[q] : kEy[q];
+      off[q] = s0 + (int64_t)s1 * L.pitch + (int64_t)kEz[q] * L.plane;
+    }
+    const int64_t lo = -guard * kChunk, hi = ncell + guard * kChunk;
+    for (int64_t i = 0; i < ncell; ++i) {
+      const int d = cmap[i];
+      if (d < 0 || (t[d] & kClassMask) != kFluid) continue;
+      const int r = row_of[i >> 2];
+      const int s = (int)i - roff[r];
+      for (int q = 1; q < kQ; ++q) {
+        const int sx = L.swap ? kEy[q] : kEx[q], sy = L.swap ? kEx[q] : kEy[q];
+        const int64_t nb = rec[(int64_t)r * 12 + (-sy + 1) * 3 + (-kEz[q] + 1)] + s - sx;
+        if (nb < lo || nb >= hi || nb < 0 || nb >= ncell || cmap[nb] != d - off[q]) {
+          c->err = "compact rows: neighbour table check failed at dense cell " + std::to_string(d) + ", q " +
+                   std::to_string(q);
+          return LBM_ERR_GEOMETRY;
+        }
+      }
+    }
+  }
+  std::vector<uint8_t> tc(ncell, 0);
+  std::vector<uint32_t> nlc(ncell, 0);
+  for (int64_t i = 0; i < ncell; ++i)
+    if (cmap[i] >= 0) {
+      tc[i] = t[cmap[i]];
+      nlc[i] = nlk[cmap[i]];
+    }
+  RCK(upload(c, &c->cmap, cmap));
+  {
+    int* p = nullptr;
+    RCK(upload(c, &p, rec));
+    c->rowrec = reinterpret_cast<int4*>(p);
+  }
+  if (c->whole.quarter) {  // one cell per lane without a list: the row record by compact group
+    std::vector<int> grec(ncell / 4 * 12);
+    for (int64_t g = 0; g < ncell / 4; ++g)
+      std::memcpy(&grec[g * 12], &rec[(int64_t)row_of[g] * 12], 12 * sizeof(int));
+    int* p = nullptr;
+    RCK(upload(c, &p, grec));
+    c->grouprec = reinterpret_cast<int4*>(p);
+  }
+  HIPCK(c, hipMalloc(&c->ctype, ncell));
+  HIPCK(c, launch_cell_gather(c->ctype, c->type, c->cmap, ncell, 1, c->s_comp));
+  uint32_t** cl[2] = {&c->clinks, &c->cnlinks};
+  const uint32_t* dl[2] = {c->links, c->nlinks};
+  for (int k = 0; k < 2; ++k) {
+    HIPCK(c, hipMalloc(cl[k], sizeof(uint32_t) * ncell));
+    HIPCK(c, launch_cell_gather(*cl[k], dl[k], c->cmap, ncell, 4, c->s_comp));
+  }
+  float** cm[4] = {&c->crho, &c->cux, &c->cuy, &c->cuz};
+  const float* dm[4] = {c->rho, c->ux, c->uy, c->uz};
+  for (int k = 0; k < 4; ++k) {
+    HIPCK(c, hipMalloc(cm[k], sizeof(float) * ncell));
+    HIPCK(c, launch_cell_gather(*cm[k], dm[k], c->cmap, ncell, 4, c->s_comp));
+  }
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  c->compact = true;
+  c->ncell_c = ncell;
+  c->nchunk_c = nchunk;
+  c->guard_c = guard;
+  // the whole domain (planes 1 .. nz) over compact cells; no slab ranges (single domain)
+  const bool quarter = c->whole.quarter;
+  free_range(c->whole);
+  free_range(c->edge);
+  free_range(c->mid);
+  const CompactView cv{&cmap, &row_of, quarter};
+  return build_range(c, c->whole, 4 * gstart[n1], 4 * gstart[(int64_t)(L.nz + 1) * n1], tc, nlc, 0, 0, &cv);
+}
+
 }  // namespace
 
 extern "C" {
@@ -732,7 +1029,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 1, 2, 64};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -820,15 +1117,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   CK(hipSetDevice(d.device));
   CK(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&c->ev_edge, &c->ev_halo, &c->ev_sum, &c->ev_fin})
+  for (hipEvent_t* e : {&c->ev_edge, &c->ev_halo, &c->ev_mid, &c->ev_fin, &c->ev_sum[0], &c->ev_sum[1]})
     CK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  {
-    // population buffers (buffer_placement(); LBM_TUNE_BUFFER_ALLOC 1: first two allocations)
-    const size_t bytes = sizeof(float) * L.buf_floats();
-    const size_t others = (size_t)L.ncell * (1 + 4 + 4 + 16 + 1) + ((size_t)1 << 30);  // type, links, macros, codes
-    CK(buffer_placement(c, bytes, others));
-    for (int b = 0; b < 2; ++b) c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
-  }
   CK(hipMalloc(&c->type, L.ncell));
   for (uint32_t** p : {&c->links, &c->nlinks}) {
     CK(hipMalloc(p, sizeof(uint32_t) * L.ncell));
@@ -943,7 +1233,9 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   // ---- work lists: whole domain, and lo edge / hi edge / interior for slabs ----
   {
     std::vector<uint8_t> t((size_t)L.ncell);
+    std::vector<uint32_t> nlk((size_t)L.ncell);
     CK(hipMemcpy(t.data(), c->type, L.ncell, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(nlk.data(), c->nlinks, sizeof(uint32_t) * L.ncell, hipMemcpyDeviceToHost));
     int64_t nf = 0;
     for (int z = 0; z < d.nz; ++z)
       for (int y = 0; y < d.ny; ++y)
@@ -983,9 +1275,14 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       }
     }
     const int64_t P = L.plane, nz = d.nz;
-    if (build_range(c, c->whole, P, (nz + 1) * P, t) != LBM_OK) return bail(LBM_ERR_HIP);
-    if (build_range(c, c->edge, P, 2 * P, t, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);
-    if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->whole, P, (nz + 1) * P, t, nlk) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->edge, P, 2 * P, t, nlk, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t, nlk) != LBM_OK) return bail(LBM_ERR_HIP);
+    // compact rows for a single domain whose step takes group lists (vessel trees)
+    if (c->d.nz_global == d.nz && !d.halo_planes && g_tune[LBM_TUNE_COMPACT] != 1 && c->whole.groups) {
+      const int rc = build_compact(c, t, nlk);
+      if (rc != LBM_OK) return bail(rc);
+    }
     // partial slots: [whole | lo | hi | mid]; the slab ranges are contiguous
     c->npart_slab = c->edge.npart + c->mid.npart;
     CK(hipMalloc(&c->partial_all, sizeof(double) * std::max(1, c->whole.npart + c->npart_slab)));
@@ -997,6 +1294,22 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     }
     c->edge.part = c->whole.part + c->whole.npart;
     c->mid.part = c->edge.part + c->edge.npart;
+  }
+  if (c->compact) {
+    // compact population buffers (small: the stored cells of a sparse lattice), zeroed
+    const size_t bytes = sizeof(float) * (size_t)(c->nchunk_c + 2 * c->guard_c) * kQ * kChunk;
+    for (int b = 0; b < 2; ++b) {
+      CK(hipMalloc(&c->alloc[b], bytes));
+      CK(hipMemsetAsync(c->alloc[b], 0, bytes, c->s_comp));
+      c->buf[b] = c->alloc[b] + c->guard_c * kQ * kChunk;
+    }
+    CK(hipStreamSynchronize(c->s_comp));
+  } else {
+    // population buffers (buffer_placement(); LBM_TUNE_BUFFER_ALLOC 1: first two allocations),
+    // allocated last: the other arrays are in place, so hipMemGetInfo counts them
+    const size_t bytes = sizeof(float) * L.buf_floats();
+    CK(buffer_placement(c, bytes, (size_t)1 << 30));
+    for (int b = 0; b < 2; ++b) c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
   }
 #undef CK
   *out = c;
@@ -1020,6 +1333,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->bc_in) (void)hipFree(c->bc_in);
   if (c->bc_out) (void)hipFree(c->bc_out);
   if (c->partial_all) (void)hipFree(c->partial_all);
+  if (c->slab_part) (void)hipFree(c->slab_part);
   if (c->red_part) (void)hipFree(c->red_part);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->conv) (void)hipFree(c->conv);
@@ -1028,8 +1342,11 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->ref_idx) (void)hipFree(c->ref_idx);
   if (c->terms) (void)hipFree(c->terms);
   if (c->cub_part) (void)hipFree(c->cub_part);
+  for (void* p : {(void*)c->cmap, (void*)c->rowrec, (void*)c->grouprec, (void*)c->ctype, (void*)c->clinks, (void*)c->cnlinks,
+                  (void*)c->crho, (void*)c->cux, (void*)c->cuy, (void*)c->cuz})
+    if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {c->ev_edge, c->ev_halo, c->ev_sum, c->ev_fin})
+  for (hipEvent_t e : {c->ev_edge, c->ev_halo, c->ev_mid, c->ev_fin, c->ev_sum[0], c->ev_sum[1]})
     if (e) (void)hipEventDestroy(e);
   if (c->s_comp) (void)hipStreamDestroy(c->s_comp);
   if (c->s_comm) (void)hipStreamDestroy(c->s_comm);
@@ -1051,8 +1368,16 @@ int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux
     HIPCK(c, hipMalloc(&dev[k], sizeof(float) * L.ncell));
     HIPCK(c, hipMemcpy(dev[k], h.data(), sizeof(float) * L.ncell, hipMemcpyHostToDevice));
   }
-  HIPCK(c, launch_init_feq(c->buf[0], c->buf[1], L.ncell, form == LBM_INIT_LDC_WI ? 0 : 1, dev[0], dev[1], dev[2],
-                           dev[3], c->s_comp));
+  Stage st;
+  float *fa = c->buf[0], *fb = c->buf[1];
+  if (c->compact) {  // evaluated on a dense copy, then gathered into both compact buffers
+    RCK(stage_dense(c, st, &fa));
+    fb = fa;
+  }
+  HIPCK(c, launch_init_feq(fa, fb, L.ncell, form == LBM_INIT_LDC_WI ? 0 : 1, dev[0], dev[1], dev[2], dev[3],
+                           c->s_comp));
+  if (c->compact)
+    for (int b = 0; b < 2; ++b) RCK(from_dense(c, fa, b));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   for (float* p : dev)
     if (p) HIPCK(c, hipFree(p));
@@ -1062,8 +1387,16 @@ int lbm_init_equilibrium(lbm_ctx* c, int form, const float* rho, const float* ux
 int lbm_init_ldc(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
-  HIPCK(c, launch_init_ldc(c->buf[0], c->buf[1], c->L.ncell, c->L.pitch, c->L.xshift, c->L.nx, c->L.ny, c->d.lid_u,
-                           c->L.swap, c->s_comp));
+  Stage st;
+  float *fa = c->buf[0], *fb = c->buf[1];
+  if (c->compact) {
+    RCK(stage_dense(c, st, &fa));
+    fb = fa;
+  }
+  HIPCK(c, launch_init_ldc(fa, fb, c->L.ncell, c->L.pitch, c->L.xshift, c->L.nx, c->L.ny, c->d.lid_u, c->L.swap,
+                           c->s_comp));
+  if (c->compact)
+    for (int b = 0; b < 2; ++b) RCK(from_dense(c, fa, b));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -1077,8 +1410,16 @@ int lbm_init_case(lbm_ctx* c) {
   }
   HIPCK(c, hipSetDevice(c->d.device));
   const Layout& L = c->L;
-  HIPCK(c, launch_init_mask(c->buf[0], c->buf[1], c->codes, c->bc_in, c->bc_out, L.nx, L.ny, L.nz, L.pitch, L.xshift,
-                            L.plane, L.ncell, c->d.z_offset, L.swap, c->s_comp));
+  Stage st;
+  float *fa = c->buf[0], *fb = c->buf[1];
+  if (c->compact) {
+    RCK(stage_dense(c, st, &fa));
+    fb = fa;
+  }
+  HIPCK(c, launch_init_mask(fa, fb, c->codes, c->bc_in, c->bc_out, L.nx, L.ny, L.nz, L.pitch, L.xshift, L.plane,
+                            L.ncell, c->d.z_offset, L.swap, c->s_comp));
+  if (c->compact)
+    for (int b = 0; b < 2; ++b) RCK(from_dense(c, fa, b));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return reset_state(c);
 }
@@ -1094,8 +1435,17 @@ int lbm_set_f(lbm_ctx* c, const float* f) {
         const float* row = f + (((int64_t)q * L.nz + z) * L.ny + y) * L.nx;
         for (int x = 0; x < L.nx; ++x) h[aidx(cell_of(L, x, y, z), q)] = row[x];
       }
-  for (int b = 0; b < 2; ++b)
-    HIPCK(c, hipMemcpy(c->buf[b], h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+  if (c->compact) {
+    Stage st;
+    float* f0 = nullptr;
+    RCK(stage_dense(c, st, &f0));
+    HIPCK(c, hipMemcpyAsync(f0, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice, c->s_comp));
+    for (int b = 0; b < 2; ++b) RCK(from_dense(c, f0, b));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+  } else {
+    for (int b = 0; b < 2; ++b)
+      HIPCK(c, hipMemcpy(c->buf[b], h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+  }
   return reset_state(c);
 }
 
@@ -1239,14 +1589,16 @@ int unpack_faces(lbm_ctx* c, int b, bool all, bool from_dn, bool from_up, hipStr
   return LBM_OK;
 }
 
-int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr) {
+// pack, send / receive and unpack the +-z faces of buffer b on s_comm (after the work already
+// queued there; after_comp: also after the work queued on s_comp)
+int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr, bool after_comp = false) {
   const size_t cnt = (size_t)(all ? kQ : 5) * c->L.plane;
   const int up = c->rank + 1 < c->nranks ? c->rank + 1 : -1;
   const int dn = c->rank > 0 ? c->rank - 1 : -1;
-  // the edge planes are done on s_comp; packing, the transfers and the unpack run on s_comm,
-  // beside the interior launch
-  HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
-  HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
+  if (after_comp) {
+    HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
+    HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
+  }
   RCK(timed(c, c->s_comm, kKindHalo, -1, -1, [&] {
     RCK(pack_faces(c, b, all, dn >= 0, up >= 0, c->s_comm));
     NCCK(c, ncclGroupStart());
@@ -1271,14 +1623,23 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     // the reference's order: per step calc_vel_square's terms into reference storage order, then
     // thrust::reduce's CUB tree in fp32 (ldc.cu:660-668)
     const Layout& L = c->L;
+    Stage st;
+    float* dense = nullptr;
+    if (c->compact) RCK(stage_dense(c, st, &dense));
     for (int s = 0; s < nsteps; ++s) {
       RCK(run_range(c, c->whole, c->cur, c->s_comp));
-      HIPCK(c, launch_vel_terms(c->buf[c->cur], c->type, c->ref_idx, c->terms, L.plane, (L.nz + 1) * L.plane, L.pitch,
-                                L.plane, L.swap, c->s_comp));
+      const float* src = c->buf[c->cur];
+      if (c->compact) {  // the terms from a dense copy (test path: one extra copy per step)
+        RCK(to_dense(c, c->cur, dense));
+        src = dense;
+      }
+      HIPCK(c, launch_vel_terms(src, c->type, c->ref_idx, c->terms, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
+                                L.swap, c->s_comp));
       c->cur ^= 1;
       HIPCK(c, launch_cub_tree(c->terms, c->n_ref, c->cub_ipt, c->cub_vec, c->cub_grid, c->cub_part, c->conv,
                                want_hist ? c->hist + s : nullptr, c->s_comp));
     }
+    if (c->compact) HIPCK(c, hipStreamSynchronize(c->s_comp));  // before the staging copy is freed
     return LBM_OK;
   }
   if (c->fuse_red && !c->conv_enabled) {
@@ -1305,32 +1666,51 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
   return LBM_OK;
 }
 
+// The slab step on two streams.  s_comp runs nothing but the interior launches, back to back;
+// everything else runs on s_comm, beside them:
+//   s_comp: [wait halo(h-1)] interior(h) -> ev_mid
+//   s_comm: edge planes(h), pack, send / recv, unpack -> ev_halo; [wait ev_mid] reduction(h) ->
+//           ev_sum[h & 1], all-reduce, finisher -> ev_fin
+// Every hazard is an event or stream order: interior(h) reads planes 1 and nz and the ghost
+// planes of src(h), which edge(h-1) and unpack(h-1) wrote (ev_halo), and overwrites src(h-1),
+// which edge(h-1) read (ev_halo); edge(h) reads planes 2 and nz-1 and overwrites planes 1 and
+// nz of src(h-1), which interior(h-1) wrote / read -- reduction(h-1), queued before edge(h),
+// waited for it.  The block partials alternate by step parity, so interior(h) only waits for
+// the reduction of step h-2 (ev_sum).  The edge launch and its halo thus overlap the interior
+// launch instead of preceding it (round 2: edge launch, interior launch and the two reduction
+// launches in series on s_comp).
 int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
   RCK(ensure_halo_buffers(c));
+  if (!c->slab_part) HIPCK(c, hipMalloc(&c->slab_part, sizeof(double) * 2 * std::max(1, c->npart_slab)));
+  // s_comm starts after whatever s_comp holds (set-up, a checkpoint load, read-outs)
+  HIPCK(c, hipEventRecord(c->ev_edge, c->s_comp));
+  HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_edge, 0));
   if (!c->halo_primed) {  // ghost planes of the initial source buffer: all 19 populations
     RCK(rccl_exchange(c, c->cur, true));
     c->halo_primed = true;
   }
   int h = c->steps_done;
   for (int s = 0; s < nsteps; ++s, ++h) {
-    HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));  // ghost planes of src(h) complete
+    const int p = h & 1;
+    double* part = c->slab_part + (size_t)p * c->npart_slab;  // [edge | interior]
+    HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_halo, 0));   // ghost and edge planes of src(h)
+    HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_sum[p], 0)); // reduction(h-2) read part
     if (c->conv_enabled) HIPCK(c, hipStreamWaitEvent(c->s_comp, c->ev_fin, 0));
-    // edge planes first, so their halo travels while the interior runs
-    RCK(run_range(c, c->edge, c->cur, c->s_comp, nullptr, kKindEdge));
+    c->last_mid_end = nullptr;
+    RCK(run_range(c, c->mid, c->cur, c->s_comp, nullptr, kKindMid, part + c->edge.npart));
+    HIPCK(c, hipEventRecord(c->ev_mid, c->s_comp));
+    RCK(run_range(c, c->edge, c->cur, c->s_comm, nullptr, kKindEdge, part));
     hipEvent_t halo_end = nullptr;
     RCK(rccl_exchange(c, c->cur ^ 1, false, &halo_end));
-    c->last_mid_end = nullptr;
-    RCK(run_range(c, c->mid, c->cur, c->s_comp, nullptr, kKindMid));
     c->cur ^= 1;
     if (c->prof && halo_end && c->last_mid_end)  // how long the halo outlasts the interior
       c->recs.push_back({c->last_mid_end, halo_end, {kKindExposed, -1, -1}});
-    // this rank's sum goes to the step-parity slot: the all-reduce of step h - 2, which read
-    // the same slot, precedes exchange(h - 1) on s_comm, and s_comp waited for that at the top
-    HIPCK(c, launch_reduce(c->edge.part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comp,
-                           &c->conv->s_slot[h & 1]));
-    HIPCK(c, hipEventRecord(c->ev_sum, c->s_comp));
-    HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_sum, 0));
-    NCCK(c, ncclAllReduce(&c->conv->s_slot[h & 1], &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
+    // this rank's sum goes to the step-parity slot of the all-reduce (the all-reduce of step
+    // h - 2, which read it, is earlier on s_comm)
+    HIPCK(c, hipStreamWaitEvent(c->s_comm, c->ev_mid, 0));
+    HIPCK(c, launch_reduce(part, c->npart_slab, c->scratch, c->conv, nullptr, 0, c->s_comm, &c->conv->s_slot[p]));
+    HIPCK(c, hipEventRecord(c->ev_sum[p], c->s_comm));
+    NCCK(c, ncclAllReduce(&c->conv->s_slot[p], &c->conv->s_global, 1, ncclDouble, ncclSum, c->comm, c->s_comm));
     HIPCK(c, launch_finish_global(c->conv, want_hist ? c->hist + s : nullptr, c->s_comm));
     HIPCK(c, hipEventRecord(c->ev_fin, c->s_comm));
   }
@@ -1360,8 +1740,8 @@ int wait_streams(lbm_ctx* c) {
   const int limit_s = g_tune[LBM_TUNE_SYNC_TIMEOUT_S];
   for (;;) {
     ncclResult_t ar = ncclSuccess;
-    if (g_tune[LBM_TUNE_INJECT_RCCL_FAULT]) {  // test hook: this wait sees a failed peer
-      g_tune[LBM_TUNE_INJECT_RCCL_FAULT] = 0;
+    if (c->inject_fault) {  // test hook (lbm_debug_fail_next_wait): this wait sees a failed peer
+      c->inject_fault = false;
       ar = ncclRemoteError;
     } else {
       const hipError_t a = hipStreamQuery(c->s_comp), b = hipStreamQuery(c->s_comm);
@@ -1396,7 +1776,12 @@ int refresh_macros(lbm_ctx* c) {
   c->macros_stale = false;
   if (h.k == 0) return LBM_OK;  // no step ran: the initial arrays
   const Layout& L = c->L;
-  const float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
+  float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
+  Stage st;
+  if (c->compact) {  // its dense copy
+    RCK(stage_dense(c, st, &src));
+    RCK(to_dense(c, c->cur ^ 1, src));
+  }
   HIPCK(c, launch_moments(src, c->type, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
                           L.swap, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
@@ -1528,7 +1913,16 @@ int lbm_get_f(lbm_ctx* c, float* f) {
   RCK(lbm_sync(c));
   const Layout& L = c->L;
   std::vector<float> h((size_t)L.nchunk * kQ * kChunk);
-  HIPCK(c, hipMemcpy(h.data(), c->buf[c->cur], sizeof(float) * h.size(), hipMemcpyDeviceToHost));
+  const float* cur = c->buf[c->cur];
+  Stage st;
+  if (c->compact) {  // the stored cells' populations into a dense copy
+    float* f = nullptr;
+    RCK(stage_dense(c, st, &f));
+    RCK(to_dense(c, c->cur, f));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+    cur = f;
+  }
+  HIPCK(c, hipMemcpy(h.data(), cur, sizeof(float) * h.size(), hipMemcpyDeviceToHost));
   for (int q = 0; q < kQ; ++q)
     for (int z = 0; z < L.nz; ++z)
       for (int y = 0; y < L.ny; ++y) {
@@ -1570,8 +1964,8 @@ int lbm_checkpoint_save(lbm_ctx* c, const char* path) {
   h.steps_done = c->steps_done; h.cur = c->cur;
   h.halo_primed = c->halo_primed ? 1 : 0;
   std::memcpy(&h.tau_bits, &c->tau, 4);
-  h.ncell = c->L.ncell;
-  h.buf_floats = c->L.nchunk * kQ * kChunk;
+  h.ncell = c->compact ? c->ncell_c : c->L.ncell;
+  h.buf_floats = c->pop_floats();
   HIPCK(c, hipMemcpy(&h.conv, c->conv, sizeof(ConvState), hipMemcpyDeviceToHost));
   std::FILE* f = std::fopen(path, "wb");
   if (!f) {
@@ -1616,7 +2010,7 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
                h.nx == c->L.nx && h.ny == c->L.ny && h.nz == c->L.nz && h.z_offset == c->d.z_offset &&
                h.nz_global == c->d.nz_global && h.case_kind == c->d.case_kind && h.swap == c->L.swap &&
                h.pitch == c->L.pitch && h.xshift == c->L.xshift && h.tau_bits == tau_bits &&
-               h.ncell == c->L.ncell && h.buf_floats == c->L.nchunk * kQ * kChunk;
+               h.ncell == (c->compact ? c->ncell_c : c->L.ncell) && h.buf_floats == c->pop_floats();
   // run state of a well-formed file: one of the two buffers current, flags 0/1, the device
   // step counter equal to the host's
   const bool sane = (h.cur == 0 || h.cur == 1) && h.steps_done >= 0 && (h.halo_primed == 0 || h.halo_primed == 1) && h.conv.k == h.steps_done &&
@@ -1695,8 +2089,17 @@ int lbm_get_launch_shape(lbm_ctx* c, int* cells_per_lane, int* main_blocks, int*
   if (!c) return LBM_ERR_ARG;
   if (cells_per_lane) *cells_per_lane = c->whole.quarter ? 1 : 4;
   if (main_blocks) *main_blocks = c->whole.main_blocks;
-  if (grid_stride) *grid_stride = c->whole.groups ? 2 : c->whole.stride ? 1 : 0;
-  if (lane_fill) *lane_fill = c->whole.groups ? c->whole.group_fill : c->whole.lane_fill;
+  const bool listless = c->compact && c->whole.quarter;
+  if (grid_stride) *grid_stride = listless ? 3 : c->whole.groups ? 2 : c->whole.stride ? 1 : 0;
+  if (lane_fill) *lane_fill = (c->whole.groups || listless) ? c->whole.group_fill : c->whole.lane_fill;
+  return LBM_OK;
+}
+
+int lbm_get_storage(lbm_ctx* c, int* compact, int64_t* cells, int64_t* bytes) {
+  if (!c) return LBM_ERR_ARG;
+  if (compact) *compact = c->compact ? 1 : 0;
+  if (cells) *cells = c->compact ? c->ncell_c : c->L.ncell;
+  if (bytes) *bytes = 2 * (int64_t)sizeof(float) * c->pop_floats();
   return LBM_OK;
 }
 
@@ -1853,6 +2256,16 @@ int lbm_comm_info(lbm_ctx* c, int* rank, int* nranks) {
   return LBM_OK;
 }
 
+int lbm_debug_fail_next_wait(lbm_ctx* c) {
+  if (!c) return LBM_ERR_ARG;
+  if (!c->comm) {
+    c->err = "lbm_debug_fail_next_wait: the context has no RCCL communicator";
+    return LBM_ERR_STATE;
+  }
+  c->inject_fault = true;
+  return LBM_OK;
+}
+
 int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nranks) {
   if (!c || !id_bytes || rank < 0 || nranks < 1 || rank >= nranks) return LBM_ERR_ARG;
   HIPCK(c, hipSetDevice(c->d.device));
@@ -1861,6 +2274,11 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
   if (c->sum_mode != LBM_SUM_FP64) {
     c->err = "lbm_attach_rccl: the reference-order residual (lbm_set_residual_order) is single-domain only";
     return LBM_ERR_ARG;
+  }
+  if (c->compact) {
+    c->err = "lbm_attach_rccl: a lattice in compact rows is a single domain (create slabs with nz_global, or "
+             "lbm_tune(LBM_TUNE_COMPACT, 1))";
+    return LBM_ERR_STATE;
   }
   NCCK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
@@ -1917,7 +2335,7 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     if (!cs[i] || cs[i]->d.device != c0->d.device || cs[i]->L.pitch != c0->L.pitch || cs[i]->L.xshift != c0->L.xshift ||
         cs[i]->L.swap != c0->L.swap || cs[i]->L.plane != c0->L.plane ||
         cs[i]->steps_done != c0->steps_done || cs[i]->cur != c0->cur || cs[i]->conv_enabled || cs[i]->comm ||
-        cs[i]->sum_mode != LBM_SUM_FP64) {
+        cs[i]->sum_mode != LBM_SUM_FP64 || cs[i]->compact) {
       c0->err = "lbm_group_step: slabs must share device, row layout (nx, ny, x_align) and step count, "
                 "without convergence control or RCCL";
       return LBM_ERR_ARG;

@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "lbm_d3q19.hpp"
 #include "lbm_kernels.hpp"
@@ -86,6 +87,72 @@ template <int Q, bool SW>
 constexpr int64_t cell_off(int pitch, int64_t plane) {
   return SDir<Q, SW>::x + row_off<Q, SW>(pitch, plane);
 }
+
+// Neighbour addressing of a lane's cell c (a 4-cell lane: its first cell):
+//   slice<Q>() -- the cell c - e_Q with e_x = 0: the aligned 16-B slice a 4-cell lane pulls,
+//   nb<Q>()    -- the cell c - e_Q.
+// AddrD: the dense box -- cell (zs, s1, s0) at s0 - xshift + s1 * pitch + zs * plane, every
+// neighbour a constant offset.  Rows: compact rows (sparse lattices, lbm_create's choice) --
+// storage row r = zs * nrow + s1 keeps only the span of its stored cells, the spans packed one
+// after the other in storage order, so cell (r, s0) lives at roff[r] + s0; a lane holds the
+// offsets of the nine rows around its own (loaded once, Rows::load).  Inside a span x +- 1 is
+// still c +- 1, and a fluid cell's neighbours are always stored, so they lie inside theirs.
+// float index of slot q of cell c (aidx): 64-bit for the dense box, 32-bit for compact rows
+// (lbm_create keeps their buffers, guards included, under 2^31 floats)
+__device__ __forceinline__ int64_t fidx(int64_t c, int q) { return aidx(c, q); }
+__device__ __forceinline__ int fidx(int c, int q) { return ((c >> 8) * kQ + q) * kChunk + (c & (kChunk - 1)); }
+
+struct AddrD {
+  int64_t c;
+  int pitch;
+  int64_t plane;
+  template <int Q, bool SW>
+  __device__ __forceinline__ int64_t slice() const { return c - row_off<Q, SW>(pitch, plane); }
+  template <int Q, bool SW>
+  __device__ __forceinline__ int64_t nb() const { return c - cell_off<Q, SW>(pitch, plane); }
+  __device__ __forceinline__ void opaque() { asm volatile("" : "+v"(c)); }
+  __device__ __forceinline__ AddrD get() const { return *this; }
+};
+template <int Q, bool SW>
+constexpr int row_k() {  // Rows::rb index of the row population Q is pulled from
+  return (-SDir<Q, SW>::y + 1) * 3 + (-SDir<Q, SW>::z + 1);
+}
+struct Rows {
+  int rb[9];  // roff[r + dy + dz * nrow], index (dy + 1) * 3 + dz + 1
+  int s0;     // the cell's position in its row: c - roff[r]
+  template <int Q, bool SW>
+  __device__ __forceinline__ int slice() const { return rb[row_k<Q, SW>()] + s0; }
+  template <int Q, bool SW>
+  __device__ __forceinline__ int nb() const { return rb[row_k<Q, SW>()] + s0 - SDir<Q, SW>::x; }
+  __device__ __forceinline__ void opaque() {
+    asm volatile("" : "+v"(rb[0]), "+v"(rb[1]), "+v"(rb[2]), "+v"(rb[3]), "+v"(rb[4]), "+v"(rb[5]), "+v"(rb[6]),
+                 "+v"(rb[7]), "+v"(rb[8]), "+v"(s0));
+  }
+  __device__ __forceinline__ Rows get() const { return *this; }
+  // the row record of row r (MainArgs::rowrec: 12 ints, the nine offsets first) -- three 16-B loads
+  __device__ __forceinline__ static Rows load(const int4* __restrict__ rowrec, int64_t c, int r) {
+    const int4* p = rowrec + (int64_t)r * 3;
+    const int4 x = p[0], y = p[1], z = p[2];
+    Rows R;
+    R.rb[0] = x.x; R.rb[1] = x.y; R.rb[2] = x.z; R.rb[3] = x.w;
+    R.rb[4] = y.x; R.rb[5] = y.y; R.rb[6] = y.z; R.rb[7] = y.w;
+    R.rb[8] = z.x;
+    R.s0 = (int)c - R.rb[4];
+    return R;
+  }
+};
+// Compact rows kept as (cell, row) until the boundary stores need them: the nine offsets are
+// loaded again there (L1 / L2 hits) instead of living in ten VGPRs across the collision
+struct RowsRef {
+  const int4* rowrec;
+  int64_t c;
+  int r;
+  __device__ __forceinline__ Rows get() const {
+    int rr = r;
+    asm volatile("" : "+v"(rr));  // a fresh load, not the pulls' values kept alive
+    return Rows::load(rowrec, c, rr);
+  }
+};
 
 // Pull of population Q for the lane's 4 cells c..c+3 from c - e_Q .. c+3 - e_Q, in two
 // phases so that all of a wave's loads are in flight together (one round trip per wave):
@@ -147,6 +214,32 @@ __device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, 
   ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], take_lo, take_hi)), ...);
 }
 
+// The same for a lane of compact 4-cell groups (GROUPS): the edge floats are the lane's own
+// neighbours, cells slice - 1 (e_x = +1) and slice + 4 (e_x = -1), in the slice's row
+template <int Q, bool SW, class A>
+__device__ __forceinline__ void pull_issue_g(f4& a, float& e, const float* __restrict__ src, const A& ad, bool need) {
+  const auto s = ad.template slice<Q, SW>();
+  const float* p = need ? src + fidx(s, Q) : src;
+  a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+  if constexpr (SDir<Q, SW>::x == 1) {
+    auto o = fidx(s - 1, Q);
+    asm volatile("" : "+v"(o));
+    e = src[o];
+  } else if constexpr (SDir<Q, SW>::x == -1) {
+    auto o = fidx(s + 4, Q);
+    asm volatile("" : "+v"(o));
+    e = src[o];
+  }
+}
+
+template <bool SW, class A, int... Qs>
+__device__ __forceinline__ void pull4_g(f4* v, const float* __restrict__ src, const A& ad, bool take_lo, bool take_hi,
+                                        bool need, std::integer_sequence<int, Qs...>) {
+  float e[kQ];
+  ((pull_issue_g<Qs, SW>(v[Qs], e[Qs], src, ad, need)), ...);
+  ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], take_lo, take_hi)), ...);
+}
+
 template <int J, int... Qs>
 __device__ __forceinline__ void relax4(f4* v, float tau, float r, float ux, float uy, float uz,
                                        std::integer_sequence<int, Qs...>) {
@@ -160,22 +253,21 @@ using AllQ = std::make_integer_sequence<int, kQ>;
 // pulls at the next step -- exactly the value boundary_stream writes there
 // (Poiseulle.cu:601-746: d_dst[q][W] = d_dst[opp q][W + e_q]).  Each wall slot has one
 // writer (W + e_q), the consumer, so the slot always lives in the writer's own storage.
-template <int Q, bool SW>
-__device__ __forceinline__ void bb_store_one(float* __restrict__ dst, int64_t c, uint32_t m, float out_opp,
-                                             int pitch, int64_t plane) {
+template <int Q, bool SW, class A>
+__device__ __forceinline__ void bb_store_one(float* __restrict__ dst, const A& ad, uint32_t m, float out_opp) {
   if constexpr (Q > 0) {
-    if (m & (1u << Q)) dst[aidx(c - cell_off<Q, SW>(pitch, plane), Q)] = out_opp;
+    if (m & (1u << Q)) dst[fidx(ad.template nb<Q, SW>(), Q)] = out_opp;
   }
 }
 // one set bit at a time (rare path: keeps the address arithmetic out of the hot registers)
-template <int J, bool SW>
-__device__ __forceinline__ void bb_store_cell(float* __restrict__ dst, int64_t c, uint32_t m, const f4* v, int pitch,
-                                              int64_t plane) {
+template <int J, bool SW, class A>
+__device__ __forceinline__ void bb_store_cell(float* __restrict__ dst, A ad, uint32_t m, const f4* v) {
 #define LBM_BB_CASE(Q) \
-  case Q: dst[aidx(c + J - cell_off<Q, SW>(pitch, plane), Q)] = v[Dir<Q>::opp][J]; break;
-  // opaque copy of c: otherwise the compiler CSEs these offsets with the pull addresses of
-  // the same directions and keeps ~70 VGPRs of them alive across the collision (240 vs 167)
-  asm volatile("" : "+v"(c));
+  case Q: dst[fidx(ad.template nb<Q, SW>() + J, Q)] = v[Dir<Q>::opp][J]; break;
+  // opaque copy of the address: otherwise the compiler CSEs these offsets with the pull
+  // addresses of the same directions and keeps ~70 VGPRs of them alive across the collision
+  // (240 vs 167)
+  ad.opaque();
   for (; m; m &= m - 1) {
     switch (__builtin_ctz(m)) {
       LBM_BB_CASE(1) LBM_BB_CASE(2) LBM_BB_CASE(3) LBM_BB_CASE(4) LBM_BB_CASE(5) LBM_BB_CASE(6)
@@ -208,9 +300,8 @@ __device__ __forceinline__ uint32_t u_from_next(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, false);
 }
 // called with the whole wave active (the DPP shifts read every lane); g: this lane's groups
-template <int Q, bool SW>
-__device__ __forceinline__ void bb_group_one(float* __restrict__ dst, int64_t c, uint32_t g, const f4* v, int pitch,
-                                             int64_t plane) {
+template <int Q, bool SW, class A>
+__device__ __forceinline__ void bb_group_one(float* __restrict__ dst, const A& ad, uint32_t g, const f4* v) {
   if constexpr (Q > 0) {
     const bool mine = (g >> Q) & 1u;
     if (__any(mine)) {  // wave-uniform
@@ -220,14 +311,14 @@ __device__ __forceinline__ void bb_group_one(float* __restrict__ dst, int64_t c,
       if constexpr (s == 0) w = o;
       else if constexpr (s == 1) w = f4{o.y, o.z, o.w, lane_from_next(o.x)};
       else w = f4{lane_from_prev(o.w), o.x, o.y, o.z};
-      if (mine) *reinterpret_cast<f4*>(dst + aidx(c - row_off<Q, SW>(pitch, plane), Q)) = w;
+      if (mine) *reinterpret_cast<f4*>(dst + fidx(ad.template slice<Q, SW>(), Q)) = w;
     }
   }
 }
-template <bool SW, int... Qs>
-__device__ __forceinline__ void bb_group_all(float* __restrict__ dst, int64_t c, uint32_t g, const f4* v, int pitch,
-                                             int64_t plane, std::integer_sequence<int, Qs...>) {
-  (bb_group_one<Qs, SW>(dst, c, g, v, pitch, plane), ...);
+template <bool SW, class A, int... Qs>
+__device__ __forceinline__ void bb_group_all(float* __restrict__ dst, const A& ad, uint32_t g, const f4* v,
+                                             std::integer_sequence<int, Qs...>) {
+  (bb_group_one<Qs, SW>(dst, ad, g, v), ...);
 }
 
 // moments (ldc.cu:316-322): sequential fp32 sum; signed sums in the reference order
@@ -379,34 +470,34 @@ struct Post1 {
     return f[Q];
   }
 };
-template <int Q, bool SW, class Src>
-__device__ __forceinline__ void nee_store_q(const MainArgs& a, int64_t c, uint32_t nl, float4 b0, float4 b1, float4 b2,
-                                            float4 b3, float4 b4, const Src& src, float r, float ux, float uy,
-                                            float uz, const Pref& p) {
+template <int Q, bool SW, class Src, class A>
+__device__ __forceinline__ void nee_store_q(const MainArgs& a, const A& ad, uint32_t nl, float4 b0, float4 b1,
+                                            float4 b2, float4 b3, float4 b4, const Src& src, float r, float ux,
+                                            float uy, float uz, const Pref& p) {
   if constexpr (Q > 0) {
     if (nl & (1u << Q)) {  // divergent only where a wave mixes faces (edges, corners)
       const int k = __builtin_popcount(nl & ((1u << Q) - 1u));  // Q's slot
-      const int64_t nb = c - cell_off<Q, SW>(a.pitch, a.plane);
+      const auto nb = ad.template nb<Q, SW>();
       float4 b;
       if (k >= kNeeSlots) b = bc_at(a, nb);
       else b = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : k == 3 ? b3 : b4;
       const float fq = src.template post<Q>(a, r, ux, uy, uz);
-      a.dst[aidx(nb, Q)] = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc, p.template of<Q>());
+      a.dst[fidx(nb, Q)] = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc, p.template of<Q>());
     }
   }
 }
 
 __device__ __forceinline__ void opaque(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 
-template <bool SW, class Src, int... Qs>
-__device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint32_t nl, BcSlots bc, const Src& src,
+template <bool SW, class Src, class A, int... Qs>
+__device__ __forceinline__ void nee_store_all(const MainArgs& a, const A& ad, uint32_t nl, BcSlots bc, const Src& src,
                                               float r, float ux, float uy, float uz, const Pref& p,
                                               std::integer_sequence<int, Qs...>) {
   // plain registers from here on: otherwise the slot selections below fold into one load at
   // a variable offset, and the records go through scratch
   float4 b0 = bc.s0, b1 = bc.s1, b2 = bc.s2, b3 = bc.s3, b4 = bc.s4;
   opaque(b0); opaque(b1); opaque(b2); opaque(b3); opaque(b4);
-  (nee_store_q<Qs, SW>(a, c, nl, b0, b1, b2, b3, b4, src, r, ux, uy, uz, p), ...);
+  (nee_store_q<Qs, SW>(a, ad, nl, b0, b1, b2, b3, b4, src, r, ux, uy, uz, p), ...);
 }
 
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
@@ -414,12 +505,16 @@ __device__ __forceinline__ void nee_store_all(const MainArgs& a, int64_t c, uint
 //        branch) the exact division, counted in exact_waves.  Both paths cost 210-218 VGPRs
 //        (two waves per SIMD) against 162-166 for the exact one alone, whose three waves per
 //        SIMD ran slower (profiles/r03_fast3_ab.log).
-template <bool FAST, bool SW, bool MASK, bool GROUPS = false>
+//  COMPACT (with GROUPS): compact rows -- the group's row record goes out beside the list
+//        entry's type byte and link masks, then the pulls (Rows).
+template <bool FAST, bool SW, bool MASK, bool GROUPS = false, bool COMPACT = false>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
+  static_assert(GROUPS || !COMPACT, "compact rows run over group lists");
   double acc = 0.0;
   int64_t c;
   bool need, take_lo, take_hi;
   f4 v[kQ];
+  RowsRef ad{};  // COMPACT: the lane's cell and row (Rows again for the bounce-back stores)
   if constexpr (GROUPS) {
     // compact groups: lane = one 4-cell group of the range's list (cb: the wave's first entry);
     // a lane takes its x-neighbours' cells from the neighbouring lane when that lane holds the
@@ -427,7 +522,8 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     // entries: the group's first cell (a multiple of 4), bit 0 set for an idle group of a
     // segment (it loads nothing); the tail lanes of the last wave read entry 0 and idle too
     const int64_t gi = cb + lane;
-    const int e = a.groups[gi < a.ngroups ? gi : 0];
+    const int64_t gs = gi < a.ngroups ? gi : 0;
+    const int e = a.groups[gs];
     need = gi < a.ngroups && !(e & 1);
     const int g = e & ~3;
     // a neighbour lane that loads nothing or holds another row position is no x-neighbour
@@ -437,7 +533,13 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     take_lo = lane == 0 || gp + 4 != g;
     take_hi = lane == 63 || gn != g + 4;
     c = g;
-    pull4_all<SW>(v, a.src, c, c + 4, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
+    if constexpr (COMPACT) {
+      const int row = a.group_row[gs];
+      pull4_g<SW>(v, a.src, Rows::load(a.rowrec, c, row), take_lo, take_hi, need, AllQ{});
+      ad = RowsRef{a.rowrec, c, row};
+    } else {
+      pull4_all<SW>(v, a.src, c, c + 4, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
+    }
   } else {
     c = cb + lane * 4;
     // lanes the chunk's mask leaves out hold no fluid cell and neighbour none: they load
@@ -491,9 +593,11 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   for (int j = 0; j < 4; ++j) {
     const unsigned t = (t4 >> (8 * j)) & 0xffu;
     const int64_t cj = c + j;
-    // NEE-adjacent cells belong to the NEE blocks of the launch (nee_cell)
+    // NEE-adjacent cells belong to the NEE blocks of the launch (nee_cell), unless the range
+    // hands the chunk waves their own slots (nee_chunks: the NEE blocks then only add the NEE
+    // neighbours' slots)
     const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
-                    !(t & kNeeAdj);
+                    (a.nee_chunks || !(t & kNeeAdj));
     if (in) {
       store |= 1u << j;
       acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
@@ -501,14 +605,15 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
   // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
-  // bounce-back slots / NEE values, and NEE-adjacent cells and cells outside the launch's
-  // ranges are stored by other threads, so those lanes store cell by cell -- sub-16-B stores
-  // cost whole partial-line writes in HBM (the x-ends of every row took 15% of the step before
-  // the xshift alignment).
+  // bounce-back slots / NEE values, and cells outside the launch's ranges (and NEE-adjacent
+  // cells the NEE blocks store) are stored by other threads, so those lanes store cell by cell
+  // -- sub-16-B stores cost whole partial-line writes in HBM (the x-ends of every row took 15%
+  // of the step before the xshift alignment), and a wave with one such lane issues both store
+  // paths (4 x 19 + 19 instructions: every y-row wave of the C3 pipe, before nee_chunks).
   const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
   const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
-  const bool keep_others = special != 0u || !lane_in || (t4 & kNee4);
+  const bool keep_others = special != 0u || !lane_in || (!a.nee_chunks && (t4 & kNee4));
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
   if (FAST && fast_wave) {
     relax_cell<0, true>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
@@ -521,6 +626,10 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     relax_cell<2, false>(v, a.tau, a.tau_rcp, r2, x2, y2, z2, AllQ{});
     relax_cell<3, false>(v, a.tau, a.tau_rcp, r3, x3, y3, z3, AllQ{});
   }
+  const auto bad = [&] {  // compact rows: the row offsets again (RowsRef)
+    if constexpr (COMPACT) return ad.get();
+    else return AddrD{c, a.pitch, a.plane};
+  }();
   if (__any(t4 & kWall4)) {  // wave-uniform: whole-group bounce-back stores (bb_group_one)
     const uint32_t b0 = (store & 1u) ? m0 : 0u, b1 = (store & 2u) ? m1 : 0u, b2 = (store & 4u) ? m2 : 0u,
                    b3 = (store & 8u) ? m3 : 0u;
@@ -530,15 +639,15 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     const uint32_t gm = pb3 & b0 & b1 & b2 & links_along<SW, -1>();  // G takes the previous lane's cell 3
     const uint32_t gpp = take_lo ? 0u : u_from_prev(gp);  // the previous lane's G holds my cell 0's wall
     const uint32_t gmn = take_hi ? 0u : u_from_next(gm);  // the next lane's G holds my cell 3's wall
-    bb_group_all<SW>(a.dst, c, g0 | gp | gm, v, a.pitch, a.plane, AllQ{});
+    bb_group_all<SW>(a.dst, bad, g0 | gp | gm, v, AllQ{});
     const uint32_t g = g0 | gp | gm;
     m0 &= ~(g0 | gm | gpp); m1 &= ~g; m2 &= ~g; m3 &= ~(g0 | gp | gmn);
   }
   if (t4 & kWall4) {  // rare, divergent: lanes holding wall-adjacent cells
-    if (store & 1u) bb_store_cell<0, SW>(a.dst, c, m0, v, a.pitch, a.plane);
-    if (store & 2u) bb_store_cell<1, SW>(a.dst, c, m1, v, a.pitch, a.plane);
-    if (store & 4u) bb_store_cell<2, SW>(a.dst, c, m2, v, a.pitch, a.plane);
-    if (store & 8u) bb_store_cell<3, SW>(a.dst, c, m3, v, a.pitch, a.plane);
+    if (store & 1u) bb_store_cell<0, SW>(a.dst, bad, m0, v);
+    if (store & 2u) bb_store_cell<1, SW>(a.dst, bad, m1, v);
+    if (store & 4u) bb_store_cell<2, SW>(a.dst, bad, m2, v);
+    if (store & 8u) bb_store_cell<3, SW>(a.dst, bad, m3, v);
   }
   float* d = a.dst + aidx(c, 0);
   if (whole) {
@@ -600,9 +709,9 @@ __device__ __forceinline__ Pref relax1(float* f, const MainArgs& a, float r, flo
 // The fast relaxation with the NEE stores fused in (waves holding NEE-adjacent cells): slot Q
 // of the NEE neighbour c - e_Q is written as soon as f_Q is relaxed, from the same feq_Q (the
 // neighbour's e_nb) -- no second equilibrium per direction, nothing kept alive for later.
-template <int Q, bool SW>
+template <int Q, bool SW, class A>
 __device__ __forceinline__ void relax_nee_q(float* f, const MainArgs& a, const Pref& p, float r, float ux, float uy,
-                                            float uz, int64_t c, uint32_t nl, float4 b0, float4 b1, float4 b2,
+                                            float uz, const A& ad, uint32_t nl, float4 b0, float4 b1, float4 b2,
                                             float4 b3, float4 b4) {
   const float pre = p.template of<Q>();
   const float fe = feq_pre<Q>(pre, ux, uy, uz);
@@ -612,7 +721,7 @@ __device__ __forceinline__ void relax_nee_q(float* f, const MainArgs& a, const P
   if constexpr (Q > 0) {
     if (nl & (1u << Q)) {
       const int k = __builtin_popcount(nl & ((1u << Q) - 1u));
-      const int64_t nb = c - cell_off<Q, SW>(a.pitch, a.plane);
+      const auto nb = ad.template nb<Q, SW>();
       float4 b;
       if (k >= kNeeSlots) b = bc_at(a, nb);
       else b = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : k == 3 ? b3 : b4;
@@ -624,25 +733,35 @@ __device__ __forceinline__ void relax_nee_q(float* f, const MainArgs& a, const P
       float e_bc;
       if constexpr (Q == 14) e_bc = feq_bc<14>(rn ? r : rb, bx, by, bz);
       else e_bc = feq_pre<Q>(rn ? pre : rb / FeqW<Q>::d, bx, by, bz);
-      a.dst[aidx(nb, Q)] = e_bc + (f[Q] - fe) * a.omc;
+      a.dst[fidx(nb, Q)] = e_bc + (f[Q] - fe) * a.omc;
     }
   }
 }
-template <bool SW, int... Qs>
+template <bool SW, class A, int... Qs>
 __device__ __forceinline__ void relax_nee_fast_all(float* f, const MainArgs& a, float r, float ux, float uy, float uz,
-                                                   int64_t c, uint32_t nl, BcSlots bc,
+                                                   const A& ad, uint32_t nl, BcSlots bc,
                                                    std::integer_sequence<int, Qs...>) {
   const Pref p(r);
   float4 b0 = bc.s0, b1 = bc.s1, b2 = bc.s2, b3 = bc.s3, b4 = bc.s4;
   opaque(b0); opaque(b1); opaque(b2); opaque(b3); opaque(b4);
-  (relax_nee_q<Qs, SW>(f, a, p, r, ux, uy, uz, c, nl, b0, b1, b2, b3, b4), ...);
+  (relax_nee_q<Qs, SW>(f, a, p, r, ux, uy, uz, ad, nl, b0, b1, b2, b3, b4), ...);
 }
 
-template <bool SW, int... Qs>
-__device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, uint32_t m,
-                                              int pitch, int64_t plane, std::integer_sequence<int, Qs...>) {
+template <bool SW, class A, int... Qs>
+__device__ __forceinline__ void fix_store_all(const float* f, float* __restrict__ dst, int64_t c, const A& ad,
+                                              uint32_t m, std::integer_sequence<int, Qs...>) {
   ((dst[aidx(c, Qs)] = f[Qs]), ...);
-  if (m) (bb_store_one<Qs, SW>(dst, c, m, f[Dir<Qs>::opp], pitch, plane), ...);
+  if (m) {
+    const auto an = ad.get();
+    (bb_store_one<Qs, SW>(dst, an, m, f[Dir<Qs>::opp]), ...);
+  }
+}
+
+// one cell's 19 plain pulls through an address policy (compact rows; NEE blocks)
+template <bool SW, class A, int... Qs>
+__device__ __forceinline__ void pull1_addr(float* f, const float* __restrict__ src, const A& ad,
+                                           std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = __builtin_nontemporal_load(src + fidx(ad.template nb<Qs, SW>(), Qs))), ...);
 }
 
 // One cell per lane (small lattices: a wave per 64 cells, so 4x the waves of the chunk path
@@ -670,9 +789,9 @@ __device__ __forceinline__ void pull1w_all(float* f, const float* __restrict__ s
 }
 
 // one cell's collision and stores once its pulls, type byte and link masks are in
-template <bool SW, bool PRE_BC = false>
-__device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, uint8_t t, uint32_t links, uint32_t nl,
-                                                float* f, BcSlots pre_bc = BcSlots{}) {
+template <bool SW, bool PRE_BC, class A>
+__device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, const A& ad, uint8_t t, uint32_t links,
+                                                uint32_t nl, float* f, BcSlots pre_bc = BcSlots{}) {
   const bool in = ((c >= a.c_lo && c < a.c_hi) || (c >= a.c_lo2 && c < a.c_hi2)) && (t & kClassMask) == kFluid;
   if (!in) return 0.0;
   // NEE-adjacent: the boundary data goes out now and arrives under the arithmetic below
@@ -689,12 +808,12 @@ __device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, ui
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   if (__any(nee) && a.tau_fast && __all(fast_div_ok1(f, rho, ux, uy, uz))) {
     // (uniform) NEE values fused into the fast relaxation; nl = 0 on the other lanes
-    relax_nee_fast_all<SW>(f, a, rho, ux, uy, uz, c, nee ? nl : 0u, bc, AllQ{});
+    relax_nee_fast_all<SW>(f, a, rho, ux, uy, uz, ad.get(), nee ? nl : 0u, bc, AllQ{});
   } else {
     const Pref pre = relax1(f, a, rho, ux, uy, uz);
-    if (nee) nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
+    if (nee) nee_store_all<SW>(a, ad.get(), nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
   }
-  fix_store_all<SW>(f, a.dst, c, (t & kWallAdj) ? links : 0u, a.pitch, a.plane, AllQ{});
+  fix_store_all<SW>(f, a.dst, c, ad, (t & kWallAdj) ? links : 0u, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
@@ -708,14 +827,15 @@ __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, i
   const uint32_t nl = a.nlinks[c];
   float f[kQ];
   pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
-  return collide_cell1<SW>(a, c, t, links, nl, f);
+  return collide_cell1<SW, false>(a, c, AddrD{c, a.pitch, a.plane}, t, links, nl, f);
 }
 
 // One cell per lane over a compact group list (sparse one-cell ranges): wave w takes the 16
 // entries 16 w .., lanes 4k .. 4k+3 the four cells of entry 16 w + k.  Idle entries (bit 0)
 // and the last wave's tail lanes point at a listed group, so their loads stay inside lines the
-// wave reads anyway; they store nothing.
-template <bool SW>
+// wave reads anyway; they store nothing.  COMPACT: compact rows (Rows), the entry's row record
+// loaded beside its type byte, then the pulls.
+template <bool SW, bool COMPACT>
 __device__ __forceinline__ double process_group_cell1(const MainArgs& a, int64_t w, int lane) {
   const int64_t gi = w * 16 + (lane >> 2);
   const int64_t gs = gi < a.ngroups ? gi : w * 16;
@@ -726,7 +846,16 @@ __device__ __forceinline__ double process_group_cell1(const MainArgs& a, int64_t
   const uint32_t links = a.links[c];
   const uint32_t nl = a.nlinks[c];
   float f[kQ];
-  pull1w_all<SW>(f, a.src, c >> 8, (int)(c & (kChunk - 1)), a.pitch, a.plane, AllQ{});  // per-lane chunk base
+  using A = std::conditional_t<COMPACT, RowsRef, AddrD>;
+  A ad;
+  if constexpr (COMPACT) {
+    const int row = a.group_row[gs];
+    pull1_addr<SW>(f, a.src, Rows::load(a.rowrec, c, row), AllQ{});
+    ad = RowsRef{a.rowrec, c, row};
+  } else {
+    ad = AddrD{c, a.pitch, a.plane};
+    pull1w_all<SW>(f, a.src, c >> 8, (int)(c & (kChunk - 1)), a.pitch, a.plane, AllQ{});  // per-lane chunk base
+  }
   // the boundary records are indexed by the list entry, so they go out with the pulls instead
   // of a round trip after the NEE-link mask (group_bc is null when the list holds no
   // NEE-adjacent cell or every record is bc_const)
@@ -738,24 +867,67 @@ __device__ __forceinline__ double process_group_cell1(const MainArgs& a, int64_t
     const float4* r = a.group_rec + ((int64_t)gb * 4 + (lane & 3)) * kNeeSlots;
     bc = BcSlots{r[0], r[1], r[2], r[3], r[4]};
   }
-  return collide_cell1<SW, true>(a, c, need ? t : (uint8_t)0, links, nl, f, bc);
+  return collide_cell1<SW, true>(a, c, ad, need ? t : (uint8_t)0, links, nl, f, bc);
 }
 
-// One NEE-adjacent fluid cell of a 4-cell range (NEE blocks, one per thread; the chunk waves
-// leave these cells alone): every static datum -- the cell id, its NEE-link mask, the boundary
-// data of its first kNeeSlots NEE neighbours -- is indexed by the list position, so it all
-// goes out in one round trip, then the 19 plain pulls and the wall links.  Collide, store the
-// cell's slots, its bounce-back slots and its NEE neighbours' slots (producer side).
+// One cell per lane over compact rows (small sparse lattices, latency-bound): wave w takes the 64
+// consecutive compact cells from (c_lo & ~63) + 64 w -- no list, so nothing precedes the first
+// round of loads: the type byte, link masks, boundary-record index and the group's row record
+// (MainArgs::grouprec, the row record of every compact group) go out together, then the pulls.
+// The walls, NEE and passive cells of the rows' spans ride along as idle lanes; a wave whose
+// lanes hold no fluid cell issues no pulls.
 template <bool SW>
+__device__ __forceinline__ double process_compact_cell1(const MainArgs& a, int64_t w, int lane) {
+  const int64_t c = (a.c_lo & ~int64_t(63)) + w * 64 + lane;
+  if (c - lane >= a.c_hi) return 0.0;  // wave-uniform: past the range
+  const int g = (int)(c >> 2);
+  const uint8_t t = a.type[c];
+  const uint32_t links = a.links[c];
+  const uint32_t nl = a.nlinks[c];
+  const int gb = a.group_bc ? a.group_bc[g] : -1;
+  const Rows R = Rows::load(a.grouprec, c, g);
+  const bool fluid = (t & kClassMask) == kFluid && c >= a.c_lo && c < a.c_hi;
+  if (!__any(fluid)) return 0.0;  // wave-uniform: walls, NEE or passive cells only
+  float f[kQ];
+  pull1_addr<SW>(f, a.src, R, AllQ{});
+  BcSlots bc{};
+  if (a.bc_uniform) {
+    bc = BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const};
+  } else if (gb >= 0) {
+    const float4* r = a.group_rec + ((int64_t)gb * 4 + (lane & 3)) * kNeeSlots;
+    bc = BcSlots{r[0], r[1], r[2], r[3], r[4]};
+  }
+  return collide_cell1<SW, true>(a, c, RowsRef{a.grouprec, c, g}, t, links, nl, f, bc);
+}
+
+// One NEE-adjacent fluid cell of a 4-cell range (NEE blocks, one per thread): every static
+// datum -- the cell id, its NEE-link mask, the boundary data of its first kNeeSlots NEE
+// neighbours -- is indexed by the list position, so it all goes out in one round trip, then
+// the 19 plain pulls and the wall links.  Collide, store the NEE neighbours' slots (producer
+// side) and, unless the chunk waves do (nee_chunks), the cell's own slots and bounce-back
+// slots.  With nee_chunks the chunk wave holding the cell collides it too, bit for bit the
+// same, and stores its slots and |u| term: lanes whose NEE-adjacent cell shares its 4-cell
+// group with other fluid cells (the pipe's rows along y) keep whole 16-B stores, and the NEE
+// work (two dependent load rounds: link mask, then boundary data) stays out of the chunk waves.
+template <bool SW, bool COMPACT>
 __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const int64_t c = a.cells[i];
   const uint32_t nl = a.cell_nl[i];
   const float4* r = a.nee_bc + (int64_t)i * kNeeSlots;
   const BcSlots bc = a.bc_uniform ? BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const}
                                   : BcSlots{r[0], r[1], r[2], r[3], r[4]};
-  const uint32_t links = a.links[c];
+  const uint32_t links = a.nee_chunks ? 0u : a.links[c];
   float f[kQ];
-  pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
+  using A = std::conditional_t<COMPACT, RowsRef, AddrD>;
+  A ad;
+  if constexpr (COMPACT) {
+    const int row = a.cell_row[i];
+    pull1_addr<SW>(f, a.src, Rows::load(a.rowrec, c, row), AllQ{});
+    ad = RowsRef{a.rowrec, c, row};
+  } else {
+    ad = AddrD{c, a.pitch, a.plane};
+    pull1_all<SW>(f, a.src, c, a.pitch, a.plane, AllQ{});
+  }
   float rho = 0.f;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) rho = rho + f[q];
@@ -763,8 +935,9 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;
   const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;
   const Pref pre = relax1(f, a, rho, ux, uy, uz);
-  nee_store_all<SW>(a, c, nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
-  fix_store_all<SW>(f, a.dst, c, links, a.pitch, a.plane, AllQ{});
+  nee_store_all<SW>(a, ad.get(), nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
+  if (a.nee_chunks) return 0.0;  // the chunk wave stores the cell and sums its |u|
+  fix_store_all<SW>(f, a.dst, c, ad, links, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
@@ -793,7 +966,8 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
   return a.chunk0 >= 0 ? (int64_t)a.chunk0 + idx : (int64_t)a.chunks[idx];
 }
 
-template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false, bool GROUPS = false>
+template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false, bool GROUPS = false,
+          bool COMPACT = false>
 __device__ __forceinline__ void step_body(const MainArgs& a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -821,23 +995,25 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
     const int idx = slot * (kBlock / 64) + wave;
-    if constexpr (QUARTER && GROUPS && STRIDE) {  // the same, grid-stride over XCD (b & 7)'s eighth
+    if constexpr (QUARTER && COMPACT) {  // one cell per lane over compact rows, no list
+      acc = process_compact_cell1<SW>(a, idx, lane);
+    } else if constexpr (QUARTER && GROUPS && STRIDE) {  // the same, grid-stride over XCD (b & 7)'s eighth
       const int64_t nw = (a.ngroups + 15) >> 4;
       const int64_t per = (nw + 7) >> 3;
       const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
       const int step = (a.main_blocks >> 3) * (kBlock / 64);
-      for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step) acc += process_group_cell1<SW>(a, i, lane);
+      for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step) acc += process_group_cell1<SW, COMPACT>(a, i, lane);
     } else if constexpr (QUARTER && GROUPS) {  // one cell per lane over the compact group list
-      if ((int64_t)idx * 16 < a.ngroups) acc = process_group_cell1<SW>(a, idx, lane);
+      if ((int64_t)idx * 16 < a.ngroups) acc = process_group_cell1<SW, COMPACT>(a, idx, lane);
     } else if constexpr (GROUPS && STRIDE) {  // compact groups, grid-stride over XCD (b & 7)'s eighth of the list
       const int64_t nw = (a.ngroups + 63) >> 6;  // 64-entry wave loads
       const int64_t per = (nw + 7) >> 3;
       const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
       const int step = (a.main_blocks >> 3) * (kBlock / 64);
       for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step)
-        acc += process_chunk<FAST, SW, false, true>(a, i * 64, lane, 0);
+        acc += process_chunk<FAST, SW, false, true, COMPACT>(a, i * 64, lane, 0);
     } else if constexpr (GROUPS) {  // compact 4-cell groups: wave idx takes list entries 64 idx ..
-      if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true>(a, (int64_t)idx * 64, lane, 0);
+      if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true, COMPACT>(a, (int64_t)idx * 64, lane, 0);
     } else if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
         acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
@@ -859,7 +1035,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     if constexpr (!QUARTER) {  // one-cell ranges have no NEE blocks
       const int w = (int)threadIdx.x >> 6;
       const int i = (bx * a.nee_waves + w) * 64 + ((int)threadIdx.x & 63);
-      if (w < a.nee_waves && i < a.n_nee) acc = nee_cell<SW>(a, i);
+      if (w < a.nee_waves && i < a.n_nee) acc = nee_cell<SW, COMPACT>(a, i);
     }
   }
   const double s = block_sum(acc, red);
@@ -867,15 +1043,16 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
 }
 
 // 4 cells per lane (big lattices): two waves per SIMD (210-253 VGPRs; one exact-division-only
-// instance runs one); MASK: the range has lane masks (sparse chunk lists)
-template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false>
+// instance runs one); MASK: the range has lane masks (sparse chunk lists); COMPACT: compact
+// rows (group lists only)
+template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false, bool COMPACT = false>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
-  step_body<FAST, false, SW, MASK, STRIDE, GROUPS>(a);
+  step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
-template <bool SW, bool GROUPS = false, bool STRIDE = false>
+template <bool SW, bool GROUPS = false, bool STRIDE = false, bool COMPACT = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_step1(const MainArgs a) {
-  step_body<false, true, SW, false, STRIDE, GROUPS>(a);
+  step_body<false, true, SW, false, STRIDE, GROUPS, COMPACT>(a);
 }
 
 // ---- residual --------------------------------------------------------------------------
@@ -958,7 +1135,7 @@ __global__ void k_unpack(float* __restrict__ f, const float* __restrict__ buf, c
 template <bool SW, int... Qs>
 __device__ __forceinline__ void prime_cell(float* f, int64_t c, uint32_t m, int pitch, int64_t plane,
                                            std::integer_sequence<int, Qs...>) {
-  (bb_store_one<Qs, SW>(f, c, m, f[aidx(c, Dir<Qs>::opp)], pitch, plane), ...);
+  (bb_store_one<Qs, SW>(f, AddrD{c, pitch, plane}, m, f[aidx(c, Dir<Qs>::opp)]), ...);
 }
 template <bool SW>
 __global__ void k_bb_prime(float* f, const uint8_t* __restrict__ type, const uint32_t* __restrict__ links,
@@ -1428,6 +1605,35 @@ __global__ void k_digest(const uint8_t* __restrict__ type, const float* __restri
   if (threadIdx.x == 0) atomicAdd(out + zl, part[0] + part[1] + part[2] + part[3]);
 }
 
+// ---- compact rows <-> the dense box ---------------------------------------------------------
+// cmap[i]: the dense cell of compact cell i (-1: a slot outside its row, which holds no cell).
+// Populations: slot q of every mapped cell, both directions; per-cell arrays: gathered.
+__global__ void k_pop_gather(float* __restrict__ dc, const float* __restrict__ sd, const int* __restrict__ cmap,
+                             int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kQ; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cell = i / kQ;
+    const int q = (int)(i - cell * kQ);
+    const int d = cmap[cell];
+    dc[aidx(cell, q)] = d >= 0 ? sd[aidx(d, q)] : 0.0f;
+  }
+}
+__global__ void k_pop_scatter(float* __restrict__ dd, const float* __restrict__ sc, const int* __restrict__ cmap,
+                              int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kQ; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cell = i / kQ;
+    const int q = (int)(i - cell * kQ);
+    const int d = cmap[cell];
+    if (d >= 0) dd[aidx(d, q)] = sc[aidx(cell, q)];
+  }
+}
+template <class T>
+__global__ void k_cell_gather(T* __restrict__ dc, const T* __restrict__ sd, const int* __restrict__ cmap, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = cmap[i];
+    dc[i] = d >= 0 ? sd[d] : T(0);
+  }
+}
+
 int grid_for(int64_t n, int block) {
   int64_t g = (n + block - 1) / block;
   if (g > 65536) g = 65536;
@@ -1476,7 +1682,20 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   const bool sw = a.swap != 0;
   Kern k;
   const size_t lds = 0;
-  if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
+  if (a.rowrec) {  // compact rows: one cell per lane without a list, or 4-cell group lists
+    if (a.quarter) {
+      if (!a.grouprec) return hipErrorInvalidValue;
+      k = sw ? k_step1<true, false, false, true> : k_step1<false, false, false, true>;
+    } else if (!a.groups) {
+      return hipErrorInvalidValue;
+    } else if (a.chunk_stride) {
+      if (a.fast_div) k = sw ? k_step<true, true, false, true, true, true> : k_step<true, false, false, true, true, true>;
+      else k = sw ? k_step<false, true, false, true, true, true> : k_step<false, false, false, true, true, true>;
+    } else {
+      if (a.fast_div) k = sw ? k_step<true, true, false, false, true, true> : k_step<true, false, false, false, true, true>;
+      else k = sw ? k_step<false, true, false, false, true, true> : k_step<false, false, false, false, true, true>;
+    }
+  } else if (a.quarter) {  // latency-bound sizes: as many resident waves as the registers allow
     if (a.groups && a.chunk_stride) k = sw ? k_step1<true, true, true> : k_step1<false, true, true>;
     else if (a.groups) k = sw ? k_step1<true, true> : k_step1<false, true>;
     else k = sw ? k_step1<true> : k_step1<false>;
@@ -1714,6 +1933,26 @@ hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux,
   const int per_plane = std::max(1, std::min(256, (int)(plane / 4096)));
   hipLaunchKernelGGL(k_digest, dim3(per_plane, nz), dim3(256), 0, s, type, rho, ux, uy, uz, nx, ny, pitch, xshift,
                      plane, z_offset, swap, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pop_compact(float* dst, const float* src, const int* cmap, int64_t n, int to_compact,
+                              hipStream_t s) {
+  const dim3 g(grid_for(n * kQ, 256));
+  if (to_compact) hipLaunchKernelGGL(k_pop_gather, g, dim3(256), 0, s, dst, src, cmap, n);
+  else hipLaunchKernelGGL(k_pop_scatter, g, dim3(256), 0, s, dst, src, cmap, n);
+  return hipGetLastError();
+}
+hipError_t launch_cell_gather(void* dst, const void* src, const int* cmap, int64_t n, int elem_bytes, hipStream_t s) {
+  const dim3 g(grid_for(n, 256));
+  if (elem_bytes == 1)
+    hipLaunchKernelGGL(k_cell_gather<uint8_t>, g, dim3(256), 0, s, static_cast<uint8_t*>(dst),
+                       static_cast<const uint8_t*>(src), cmap, n);
+  else if (elem_bytes == 4)
+    hipLaunchKernelGGL(k_cell_gather<uint32_t>, g, dim3(256), 0, s, static_cast<uint32_t*>(dst),
+                       static_cast<const uint32_t*>(src), cmap, n);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -104,9 +104,22 @@ struct MainArgs {
   const float4* nee_bc;     // kNeeSlots records per cell: the boundary data of its first NEE
                             // directions, gathered once (static)
   int n_nee;
+  int nee_chunks;           // 1: the chunk waves also collide and store the NEE-adjacent cells (their
+                            // own and bounce-back slots, |u|); the NEE blocks add only the NEE values
   int nee_blocks;           // multiple of 8 (keeps the chunk blocks' XCD order)
   int nee_waves;            // active waves per NEE block (1 for short, scattered lists)
   int swap;             // 1: storage rows run along physical y (Layout::swap)
+  // Compact rows (nullable; sparse single-domain lattices, group lists only): every per-cell
+  // array above and the population buffers are indexed by compact cell ids -- storage row
+  // r = zs * rows_per_plane + s1 keeps only the span of its stored cells, packed in storage
+  // order, cell (r, s0) at roff[r] + s0.  rowrec[r]: 12 ints, roff[r + dy + dz * rows_per_plane]
+  // at index (dy + 1) * 3 + dz + 1 (dy, dz in -1..1).
+  const int4* rowrec;
+  const int* group_row;  // the storage row of every group-list entry
+  const int4* grouprec;  // one-cell compact ranges (no list): the row record of every compact
+                         // 4-cell group (3 x int4, rowrec's layout); group_bc is then indexed by
+                         // compact group
+  const int* cell_row;   // the storage row of every NEE-block cell
   // The previous step's residual inside this launch (single domain, one cell per lane, no
   // convergence control): red_blocks (0 or 8) extra blocks lead the grid; the first sums
   // red_partial[0 .. red_n) -- the partials of the previous step's launch, complete at this
@@ -196,6 +209,13 @@ hipError_t launch_probe_copy(const void* src, void* dst, int64_t n4, int blocks,
 // zero n4 16-B vectors with one sweep of non-temporal stores (one region per XCD): the write
 // rate buffer_placement ranks allocations by
 hipError_t launch_probe_fill(void* dst, int64_t n4, hipStream_t s);
+
+// compact rows (MainArgs::rowrec): cmap[i] = the dense cell of compact cell i, or -1.
+// Populations of the n compact cells from a dense buffer (to_compact = 1; unmapped slots 0) or
+// back into one (0; unmapped slots skipped).  Per-cell arrays (1- or 4-byte elements) gathered.
+hipError_t launch_pop_compact(float* dst, const float* src, const int* cmap, int64_t n, int to_compact,
+                              hipStream_t s);
+hipError_t launch_cell_gather(void* dst, const void* src, const int* cmap, int64_t n, int elem_bytes, hipStream_t s);
 
 // halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack
 hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const int* qs_dev, int nq,

@@ -34,7 +34,7 @@ LBM_INIT_LDC_WI, LBM_INIT_EXPANDED = 0, 1
 LBM_SUM_FP64, LBM_SUM_CUB_TREE = 0, 1  # lbm_set_residual_order
 # lbm_tune knobs (include/lbm.h lbm_tune_knob)
 (TUNE_ROW_AXIS, TUNE_CELLS_PER_LANE, TUNE_EXACT_DIV, TUNE_FUSED_RESIDUAL, TUNE_BUFFER_ALLOC,
- TUNE_SYNC_TIMEOUT_S, TUNE_GRID_STRIDE, TUNE_INJECT_RCCL_FAULT, TUNE_GROUPS, TUNE_GROUP_SEGMENT) = range(10)
+ TUNE_SYNC_TIMEOUT_S, TUNE_GRID_STRIDE, TUNE_INJECT_RCCL_FAULT, TUNE_GROUPS, TUNE_GROUP_SEGMENT, TUNE_COMPACT) = range(11)
 
 # reference per-case constants
 LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55
@@ -85,9 +85,9 @@ class lbm_desc(C.Structure):
 LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_tune", "lbm_get_nonfinite", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_set_residual_order", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
-    "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_numerics",
+    "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_storage", "lbm_get_numerics",
     "lbm_get_layout", "lbm_get_launch_shape", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
-    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
+    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_debug_fail_next_wait", "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
 ]
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
@@ -181,6 +181,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_stats": (C.c_int, [P, f64p, i64p, f64p]),
             "lbm_kernel_times": (C.c_int, [P, C.c_int, f64p, i64p]),
             "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
+            "lbm_get_storage": (C.c_int, [P, ip, i64p, i64p]),
             "lbm_checkpoint_save": (C.c_int, [P, C.c_char_p]),
             "lbm_checkpoint_load": (C.c_int, [P, C.c_char_p]),
             "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
@@ -190,6 +191,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_comm_info": (C.c_int, [P, ip, ip]),
+            "lbm_debug_fail_next_wait": (C.c_int, [P]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
             "lbm_probe_stream": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p]),
             "lbm_probe_stream_shapes": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p, C.c_int, ip]),
@@ -202,6 +204,21 @@ def lbm_lib() -> C.CDLL:
             fn.restype, fn.argtypes = res, args
         _lbm = L
     return _lbm
+
+
+def kernel_fingerprint() -> str:
+    """16 hex digits identifying the code of liblbm's kernels and launch logic: sha256 of
+    csrc/lbm_kernels.hip, lbm_kernels.hpp, lbm_d3q19.hpp and lbm_ctx.hip with // comments and
+    whitespace removed.  Profiles record it (tools/pmc_*.py) so that bench.py reports measured
+    HBM traffic only next to the kernels it was measured on."""
+    import hashlib
+    import re
+    h = hashlib.sha256()
+    for name in ("lbm_kernels.hip", "lbm_kernels.hpp", "lbm_d3q19.hpp", "lbm_ctx.hip"):
+        text = open(os.path.join(ROOT, "csrc", name)).read()
+        text = re.sub(r"//[^\n]*", "", text)
+        h.update(re.sub(r"\s+", "", text).encode())
+    return h.hexdigest()[:16]
 
 
 def version() -> str:
@@ -550,6 +567,12 @@ class Lattice:
                  "lbm_get_layout")
         return {"row_axis": ra.value, "pitch": pitch.value, "x_align": xa.value, "active_chunks": nch.value}
 
+    def storage(self):
+        """Population storage: compact rows or the dense box, cell slots per buffer, bytes of both."""
+        cm, cells, by = C.c_int(), C.c_int64(), C.c_int64()
+        self._ck(lbm_lib().lbm_get_storage(self.h, C.byref(cm), C.byref(cells), C.byref(by)), "lbm_get_storage")
+        return {"compact": bool(cm.value), "cells": cells.value, "bytes": by.value}
+
     def launch_shape(self):
         """How the step kernel covers the chunks: cells per lane, chunk workgroups, whether they
         loop over their XCD's chunks (grid stride), mean share of busy chunk lanes."""
@@ -591,6 +614,10 @@ class Lattice:
         r, n = C.c_int(), C.c_int()
         self._ck(lbm_lib().lbm_comm_info(self.h, C.byref(r), C.byref(n)), "lbm_comm_info")
         return r.value, n.value
+
+    def debug_fail_next_wait(self):
+        """Test hook: this context's next wait sees a failed RCCL peer (lbm_debug_fail_next_wait)."""
+        self._ck(lbm_lib().lbm_debug_fail_next_wait(self.h), "lbm_debug_fail_next_wait")
 
     def attach_rccl(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

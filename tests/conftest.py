@@ -51,14 +51,18 @@ def knob(lbm):
         lbm.tune(which, prev)
 
 
-@pytest.fixture(params=["4", "4g", "1", "1g"], ids=["4cells", "4groups", "1cell", "1groups"])
+@pytest.fixture(params=["4", "4g", "4c", "1", "1g", "1c"],
+                ids=["4cells", "4groups", "4compact", "1cell", "1groups", "1compact"])
 def cells_per_lane(request, knob, lbm):
     """Run a parity test through every stream-collide path: four cells per lane over whole
     chunks (the bandwidth path), four cells per lane over compact lists of active 4-cell groups
-    (sparse lattices; forced on every sparse chunk list), one cell per lane over whole chunks
-    (what small lattices use by default) and one cell per lane over the group lists."""
+    (sparse lattices; forced on every sparse chunk list) in the dense box and in compact rows
+    (LBM_TUNE_COMPACT 2: single-domain lattices whose list is sparse), one cell per lane over whole
+    chunks (what small lattices use by default) and one cell per lane over the group lists, dense
+    and compact."""
     knob(lbm.TUNE_CELLS_PER_LANE, 4 if request.param.startswith("4") else 1)
-    knob(lbm.TUNE_GROUPS, 2 if request.param.endswith("g") else 1)
+    knob(lbm.TUNE_GROUPS, 1 if len(request.param) == 1 else 2)
+    knob(lbm.TUNE_COMPACT, 2 if request.param.endswith("c") else 1)
     return 4 if request.param.startswith("4") else 1
 
 

@@ -28,6 +28,13 @@ def vessel_mask(shape, seed, nballs=5):
     return m
 
 
+def stored_cells(geo):
+    """Cells whose populations are defined in every storage mode: fluid, walls and boundary
+    cells.  Compact rows (LBM_TUNE_COMPACT) keep no slots for the passive cells outside the row
+    spans, which lbm_get_f then reports as 0; lbm.h defines only the fluid cells' values."""
+    return (geo != 0) & (geo != -1)
+
+
 def inlet_tables(shape, seed):
     nz, ny, nx = shape
     rng = np.random.default_rng(seed)
@@ -205,7 +212,7 @@ def test_groups_bitwise(gpu, knob, case):
             lat = build()
         shape = lat.launch_shape()
         hist = lat.step(12)
-        f = lat.f()
+        f = lat.f()[:, stored_cells(lat.geo())]
         lat.close()
         return shape, f, hist
 
@@ -222,9 +229,10 @@ def test_groups_bitwise(gpu, knob, case):
 @pytest.mark.parametrize("case", ["coronary", "bif"])
 def test_one_cell_groups_default_bitwise(gpu, knob, case):
     """A sparse list with few active groups (the coronary tree; C4, whose 391 chunks are one-cell
-    size anyway) runs one cell per lane over the compact group list by default.  Forcing four
-    cells per lane over the same list, or one cell per lane over whole chunks, changes only
-    which lane updates which cell: populations bit for bit equal."""
+    size anyway) runs one cell per lane by default, over consecutive cells of its compact rows.
+    Forcing four cells per lane over the compact group list, or one cell per lane over whole
+    chunks of the dense box, changes only which lane updates which cell: populations bit for
+    bit equal."""
     from lbm_amd import cases
 
     def build():
@@ -237,14 +245,65 @@ def test_one_cell_groups_default_bitwise(gpu, knob, case):
             lat = build()
         shape = lat.launch_shape()
         hist = lat.step(12)
-        f = lat.f()
+        f = lat.f()[:, stored_cells(lat.geo())]
         lat.close()
         return shape, f, hist
 
-    s0, f0, h0 = run(0, 0)
-    assert s0["cells_per_lane"] == 1 and s0["grid_stride"] == 2, s0
+    s0, f0, h0 = run(0, 0)  # compact rows, one cell per lane, no list (LBM_TUNE_COMPACT auto)
+    assert s0["cells_per_lane"] == 1 and s0["grid_stride"] == 3, s0
     for cpl, groups, want in ((4, 2, (4, 2)), (1, 1, (1, 0))):
         s, f, h = run(cpl, groups)
         assert (s["cells_per_lane"], s["grid_stride"]) == want, (cpl, groups, s)
         assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), (case, cpl, groups)
         assert np.all(np.isfinite(h)) and np.allclose(h, h0, rtol=0, atol=2e-7), (h, h0)
+
+
+@pytest.mark.parametrize("case", ["bif", "bif_x2_device", "coronary", "vessel_x"])
+def test_compact_rows_vs_dense(gpu, knob, case, tmp_path):
+    """Compact rows (LBM_TUNE_COMPACT, the default for sparse single-domain lattices: every
+    storage row keeps only the span of its stored cells) against the dense box: the same fields
+    and populations bit for bit after stepping, residuals to one fp32 ulp of S (the |u| partials
+    are summed per launch block, and the blocks differ), a checkpoint resumed bit for bit, and
+    the buffers a fraction of the box."""
+    from lbm_amd import cases
+    import lbm_amd
+
+    def make(compact):
+        # the bifurcations take compact rows by default (auto); the small trees are forced
+        # onto group lists (LBM_TUNE_GROUPS 2) and compact rows (LBM_TUNE_COMPACT 2)
+        forced = case in ("coronary", "vessel_x")
+        knob(lbm_amd.TUNE_GROUPS, 2 if forced else 0)
+        knob(lbm_amd.TUNE_COMPACT, (2 if forced else 0) if compact else 1)
+        if case == "bif":
+            return cases.bifurcation(1)[0]
+        if case == "bif_x2_device":
+            return cases.bifurcation_upsampled(2)[0]
+        if case == "coronary":
+            return cases.coronary(*cases.coronary_small_vessel())[0]
+        return cases.mask_device(np.ascontiguousarray(vessel_mask((30, 40, 66), 3).transpose(0, 2, 1)))
+
+    a, b = make(True), make(False)
+    sa, sb = a.storage(), b.storage()
+    assert sa["compact"] and not sb["compact"], (sa, sb)
+    assert sa["cells"] < 0.6 * sb["cells"], (sa, sb)
+    ha, hb = a.step(25), b.step(25)
+    np.testing.assert_allclose(np.asarray(ha, np.float64), np.asarray(hb, np.float64), rtol=0, atol=1.2e-7)
+    geo = b.geo()
+    fl = geo == 4
+    for x, y in zip(a.macros(), b.macros()):
+        assert np.array_equal(x[fl].view(np.uint32), y[fl].view(np.uint32))
+    fa, fb = a.f(), b.f()
+    assert np.array_equal(fa[:, fl].view(np.uint32), fb[:, fl].view(np.uint32))
+    path = str(tmp_path / "compact.ckpt")
+    a.checkpoint_save(path)
+    ha2 = a.step(10)
+    c = make(True)
+    c.checkpoint_load(path)
+    hc = c.step(10)
+    assert np.array_equal(ha2.view(np.uint32), hc.view(np.uint32))
+    for x, y in zip(a.macros(), c.macros()):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    with pytest.raises(lbm_amd.LbmError):  # a compact lattice is a single domain
+        a.attach_rccl(lbm_amd.rccl_unique_id(), 0, 1)
+    for lat in (a, b, c):
+        lat.close()

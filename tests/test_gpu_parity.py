@@ -481,7 +481,7 @@ def test_north_star_512_bitwise(gpu, oracle):
 
 def test_rccl_abort_is_sticky(gpu, knob):
     """A wait that sees a failed peer aborts the communicator (here injected with
-    LBM_TUNE_INJECT_RCCL_FAULT on a one-rank RCCL slab).  From then on the context refuses to
+    lbm_debug_fail_next_wait on a one-rank RCCL slab; a second context is not affected).  From then on the context refuses to
     step, wait, read out or checkpoint with LBM_ERR_RCCL -- it does not fall back to stepping
     the slab as a single domain with stale ghost planes."""
     from lbm_amd import cases, LbmError
@@ -491,10 +491,15 @@ def test_rccl_abort_is_sticky(gpu, knob):
     lat.step(3)
     lat.step(2, history=False)
     lat.sync()  # streams drained: the abort below finds no work in flight
-    knob(lbm_amd.TUNE_INJECT_RCCL_FAULT, 1)
+    other = cases.ldc_device(16, 16, 16)
+    other.attach_rccl(lbm_amd.rccl_unique_id(), 0, 1)
+    lat.debug_fail_next_wait()
+    other.step(2)
+    other.sync()  # the hook is per context: this one waits normally
     with pytest.raises(LbmError, match="RCCL peer failure"):
         lat.sync()
-    assert lbm_amd.tune(lbm_amd.TUNE_INJECT_RCCL_FAULT, 0) == 0  # the hook fired once and reset
+    other.step(1)
+    other.close()
     for call in (lambda: lat.step(1), lat.sync, lat.macros, lat.state, lat.comm_info, lat.f,
                  lambda: lat.checkpoint_save("/tmp/never_written.bin")):
         with pytest.raises(LbmError, match="aborted"):

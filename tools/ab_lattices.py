@@ -47,7 +47,9 @@ def child(which):
 
     out = {}
     for w in which.split(","):
-        if w.startswith("ldc"):
+        if w == "c5":  # the C5 lattice (512 x 512 x 4096, ~187 GB) as one domain
+            out[w] = run(cases.ldc_device(512, 512, 4096), 10)
+        elif w.startswith("ldc"):
             n = int(w[3:])
             out[w] = run(cases.ldc_device(n, n, n), 2000 if n <= 64 else 200 if n <= 256 else 30)
         elif w == "c3":
@@ -58,6 +60,7 @@ def child(which):
             out[w] = run(cases.bifurcation_upsampled(4)[0], 300)
         elif w == "coronary":
             out[w] = run(cases.coronary(cases.coronary_reference_vessel())[0], 1000)
+    out["kernel_src"] = lbm_amd.kernel_fingerprint()
     print("AB " + json.dumps(out), flush=True)
 
 
@@ -82,6 +85,7 @@ def main():
                 print(f"{v} round {r}: rc {p.returncode}\n{p.stderr[-2000:]}", flush=True)
                 sys.exit(1)
             d = json.loads(line[0][3:])
+            d.pop("kernel_src", None)
             res[v].append(d)
             print(f"round {r} {v:16s} " + "  ".join(f"{k} {x['us_step']:.2f}/{x['k_step_us']:.2f}" for k, x in d.items()),
                   flush=True)

@@ -17,7 +17,8 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {"c3": "poiseuille_128x512x128 (C3)", "c4": "bifurcation_64x83x32 (C4)",
          "c4x4": "bifurcation_x4_256x332x128 (C4 upsampled)", "coronary": "coronary_291x291x372 (synthetic vessel)",
-         "ldc64": "ldc_64^3", "ldc256": "ldc_256^3 (C2)", "ldc512": "ldc_512^3"}
+         "ldc64": "ldc_64^3", "ldc256": "ldc_256^3 (C2)", "ldc512": "ldc_512^3",
+         "c5": "ldc_512x512x4096 (C5 lattice)"}
 
 
 def counters(path):
@@ -37,7 +38,8 @@ def main():
         d = os.path.join(src, case)
         if not os.path.isdir(d):
             continue
-        ab = [json.loads(ln[3:]) for ln in open(os.path.join(d, "kt.json")) if ln.startswith("AB ")][0][case]
+        abl = [json.loads(ln[3:]) for ln in open(os.path.join(d, "kt.json")) if ln.startswith("AB ")][0]
+        ab = abl[case]
         kt = [r for r in csv.DictReader(open(glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))[0]))
               if "k_step" in r["Name"]]
         calls = sum(int(r["Calls"]) for r in kt)
@@ -55,7 +57,7 @@ def main():
             "achieved_algo_gbs": round(algo / avg_ns, 1) if avg_ns else None,
             "frac_of_8tbs": round(algo / avg_ns / 8000.0, 4) if avg_ns else None,
             "sq_per_launch": {k: round(v, 1) for k, v in sorted(sq.items())},
-            "tag": tag,
+            "tag": tag, "kernel_src": abl.get("kernel_src"),
         }
         print(case, json.dumps(out[case]))
     with open(os.path.join(REPO, "profiles", f"{tag}_lattices.json"), "w") as f:

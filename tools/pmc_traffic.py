@@ -72,9 +72,13 @@ def main():
         out[name] = {"kernel": k, "dispatches": n, "read_bytes": int(rd), "write_bytes": int(wr),
                      "bytes_per_launch": int(rd + wr), "avg_duration_ns": dur}
     wl = os.environ.get("LBM_WORKLOAD", "ldc_512x512x512_per_gpu")
+    ksrc = None  # the bench line of the kernel-trace pass names the kernels it ran
+    for ln in open(os.path.join(src, "kt.log")):
+        if ln.startswith("{") and '"kernel_src"' in ln:
+            ksrc = json.loads(ln)["kernel_src"]
     path = os.path.join(prof, "pmc_traffic.json")
     d = json.load(open(path)) if os.path.exists(path) else {}
-    d[wl] = dict(out.get(MAIN, {}), tag=tag, reduce=out.get(FIX),
+    d[wl] = dict(out.get(MAIN, {}), tag=tag, kernel_src=ksrc, reduce=out.get(FIX),
                  note="FETCH_SIZE x2 (gfx950 half-count of 16-B/lane streaming reads) + WRITE_SIZE, KiB->B; "
                       "separate --pmc passes of bench.py --steps 20 --warmup 5")
     json.dump(d, open(path, "w"), indent=1)
