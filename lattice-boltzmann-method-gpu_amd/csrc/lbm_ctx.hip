@@ -166,6 +166,12 @@ struct lbm_ctx {
   float *crho = nullptr, *cux = nullptr, *cuy = nullptr, *cuz = nullptr;
   // slots per population buffer past the leading guard (the part checkpoints hold)
   int64_t pop_floats() const { return (compact ? nchunk_c : L.nchunk) * kQ * kChunk; }
+  // bounce-back on the consumer side (MainArgs::bb_pull): one-cell compact ranges read a wall
+  // link's value from the cell's own opposite slot, so no step writes wall slots
+  bool bb_pull() const { return compact && whole.quarter; }
+  // step k's source buffer holds wall slots that must be pulled raw (MainArgs::bb_raw): the
+  // first step of a case whose walls do not bounce back at step 0
+  bool bb_raw(int k) const { return k == 0 && !bb_immediate; }
   std::string err;
 };
 
@@ -351,9 +357,11 @@ void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
 
 // one step of a range from buffer srcbuf into srcbuf ^ 1
 int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* fr = nullptr, int range_kind = -1,
-              double* part = nullptr) {
+              double* part = nullptr, int step = -1) {
   MainArgs a{};
   fill_main_args(c, a, srcbuf);
+  a.bb_pull = (c->compact && r.quarter) ? 1 : 0;
+  a.bb_raw = c->bb_raw(step) ? 1 : 0;
   a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
@@ -1627,14 +1635,16 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     float* dense = nullptr;
     if (c->compact) RCK(stage_dense(c, st, &dense));
     for (int s = 0; s < nsteps; ++s) {
-      RCK(run_range(c, c->whole, c->cur, c->s_comp));
+      const int k = c->steps_done + s;
+      RCK(run_range(c, c->whole, c->cur, c->s_comp, nullptr, -1, nullptr, k));
       const float* src = c->buf[c->cur];
       if (c->compact) {  // the terms from a dense copy (test path: one extra copy per step)
         RCK(to_dense(c, c->cur, dense));
         src = dense;
       }
-      HIPCK(c, launch_vel_terms(src, c->type, c->ref_idx, c->terms, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
-                                L.swap, c->s_comp));
+      const uint32_t* bbl = (c->bb_pull() && !c->bb_raw(k)) ? c->links : nullptr;
+      HIPCK(c, launch_vel_terms(src, c->type, bbl, c->ref_idx, c->terms, L.plane, (L.nz + 1) * L.plane, L.pitch,
+                                L.plane, L.swap, c->s_comp));
       c->cur ^= 1;
       HIPCK(c, launch_cub_tree(c->terms, c->n_ref, c->cub_ipt, c->cub_vec, c->cub_grid, c->cub_part, c->conv,
                                want_hist ? c->hist + s : nullptr, c->s_comp));
@@ -1649,7 +1659,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     for (int s = 0; s < nsteps; ++s) {
       double* part = c->red_part + (size_t)(s & 1) * c->red_n;
       const FusedRed fr{part, prev, (want_hist && s > 0) ? c->hist + s - 1 : nullptr};
-      RCK(run_range(c, c->whole, c->cur, c->s_comp, &fr));
+      RCK(run_range(c, c->whole, c->cur, c->s_comp, &fr, -1, nullptr, c->steps_done + s));
       c->cur ^= 1;
       prev = part;
     }
@@ -1658,7 +1668,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     return LBM_OK;
   }
   for (int s = 0; s < nsteps; ++s) {
-    RCK(run_range(c, c->whole, c->cur, c->s_comp));
+    RCK(run_range(c, c->whole, c->cur, c->s_comp, nullptr, -1, nullptr, c->steps_done + s));
     c->cur ^= 1;
     HIPCK(c, launch_reduce(c->whole.part, c->whole.npart, c->scratch, c->conv, want_hist ? c->hist + s : nullptr,
                            1, c->s_comp));
@@ -1782,8 +1792,10 @@ int refresh_macros(lbm_ctx* c) {
     RCK(stage_dense(c, st, &src));
     RCK(to_dense(c, c->cur ^ 1, src));
   }
-  HIPCK(c, launch_moments(src, c->type, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch, L.plane,
-                          L.swap, c->s_comp));
+  // the last step ran from this buffer: step h.k - 1
+  const uint32_t* bbl = (c->bb_pull() && !c->bb_raw(h.k - 1)) ? c->links : nullptr;
+  HIPCK(c, launch_moments(src, c->type, bbl, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch,
+                          L.plane, L.swap, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return LBM_OK;
 }

@@ -763,6 +763,16 @@ __device__ __forceinline__ void pull1_addr(float* f, const float* __restrict__ s
                                            std::integer_sequence<int, Qs...>) {
   ((f[Qs] = __builtin_nontemporal_load(src + fidx(ad.template nb<Qs, SW>(), Qs))), ...);
 }
+// the same with bounce-back on the consumer side (MainArgs::bb_pull): where bit q of wl is set
+// (c - e_q a wall), population q comes from the cell's own slot opp(q) -- Poiseulle.cu:601-746's
+// d_dst[q][W] = d_dst[opp q][W + e_q] with W + e_q = c, read where it was stored
+template <bool SW, class A, int... Qs>
+__device__ __forceinline__ void pull1_bb(float* f, const float* __restrict__ src, const A& ad, int c, uint32_t wl,
+                                         std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = __builtin_nontemporal_load(
+        src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp) : fidx(ad.template nb<Qs, SW>(), Qs)))),
+   ...);
+}
 
 // One cell per lane (small lattices: a wave per 64 cells, so 4x the waves of the chunk path
 // and a quarter of its per-wave latency): plain pulls, exact division, bounce-back slots.
@@ -889,7 +899,9 @@ __device__ __forceinline__ double process_compact_cell1(const MainArgs& a, int64
   const bool fluid = (t & kClassMask) == kFluid && c >= a.c_lo && c < a.c_hi;
   if (!__any(fluid)) return 0.0;  // wave-uniform: walls, NEE or passive cells only
   float f[kQ];
-  pull1_addr<SW>(f, a.src, R, AllQ{});
+  // consumer-side bounce-back: the wall links select the cell's own slots (no wall stores below)
+  const uint32_t wl = (a.bb_pull && !a.bb_raw && fluid && (t & kWallAdj)) ? links : 0u;
+  pull1_bb<SW>(f, a.src, R, (int)c, wl, AllQ{});
   BcSlots bc{};
   if (a.bc_uniform) {
     bc = BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const};
@@ -897,7 +909,7 @@ __device__ __forceinline__ double process_compact_cell1(const MainArgs& a, int64
     const float4* r = a.group_rec + ((int64_t)gb * 4 + (lane & 3)) * kNeeSlots;
     bc = BcSlots{r[0], r[1], r[2], r[3], r[4]};
   }
-  return collide_cell1<SW, true>(a, c, RowsRef{a.grouprec, c, g}, t, links, nl, f, bc);
+  return collide_cell1<SW, true>(a, c, RowsRef{a.grouprec, c, g}, t, a.bb_pull ? 0u : links, nl, f, bc);
 }
 
 // One NEE-adjacent fluid cell of a 4-cell range (NEE blocks, one per thread): every static
@@ -1447,14 +1459,21 @@ __global__ void k_init_ldc(float* fa, float* fb, int64_t n, int pitch, int xshif
 // pattern): the same 19 pulls and the same fp32 sums as process_chunk / process_cell1, so
 // the bits are those the step used (NEE values included: they sit in the boundary cells'
 // slots of that buffer, stored there by the step before).
+// bb_links (nullable): consumer-side bounce-back (MainArgs::bb_pull) -- wall-linked populations
+// from the cell's own opposite slots
+template <bool SW, int... Qs>
+__device__ __forceinline__ void pull1_links(float* f, const float* __restrict__ src, int64_t c, uint32_t wl, int pitch,
+                                            int64_t plane, std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = src[(wl >> Qs) & 1u ? aidx(c, Dir<Qs>::opp) : aidx(c - cell_off<Qs, SW>(pitch, plane), Qs)]), ...);
+}
 template <bool SW>
-__global__ void k_moments(const float* __restrict__ src, const uint8_t* __restrict__ type, float* rho, float* ux,
-                          float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane) {
+__global__ void k_moments(const float* __restrict__ src, const uint8_t* __restrict__ type, const uint32_t* bb_links,
+                          float* rho, float* ux, float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane) {
   for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
     const uint8_t t = type[c];
     if ((t & kClassMask) != kFluid) continue;
     float f[kQ];
-    pull1_all<SW>(f, src, c, pitch, plane, AllQ{});
+    pull1_links<SW>(f, src, c, (bb_links && (t & kWallAdj)) ? bb_links[c] : 0u, pitch, plane, AllQ{});
     float r = 0.f;
 #pragma unroll
     for (int q = 0; q < kQ; ++q) r = r + f[q];
@@ -1469,13 +1488,14 @@ __global__ void k_moments(const float* __restrict__ src, const uint8_t* __restri
 // calc_vel_square (ldc.cu:460-466): the step's |u| per fluid cell -- from the step's source
 // buffer, the same pulls and sums as the step (k_moments) -- into its reference storage slot
 template <bool SW>
-__global__ void k_vel_terms(const float* __restrict__ src, const uint8_t* __restrict__ type,
+__global__ void k_vel_terms(const float* __restrict__ src, const uint8_t* __restrict__ type, const uint32_t* bb_links,
                             const int* __restrict__ ref_idx, float* __restrict__ terms, int64_t lo, int64_t hi,
                             int pitch, int64_t plane) {
   for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
-    if ((type[c] & kClassMask) != kFluid) continue;
+    const uint8_t t = type[c];
+    if ((t & kClassMask) != kFluid) continue;
     float f[kQ];
-    pull1_all<SW>(f, src, c, pitch, plane, AllQ{});
+    pull1_links<SW>(f, src, c, (bb_links && (t & kWallAdj)) ? bb_links[c] : 0u, pitch, plane, AllQ{});
     float r = 0.f;
 #pragma unroll
     for (int q = 0; q < kQ; ++q) r = r + f[q];
@@ -1896,21 +1916,27 @@ hipError_t launch_nee_gather(const int* cells, const uint32_t* nl, const float* 
   return hipGetLastError();
 }
 
-hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
-                          int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
+hipError_t launch_moments(const float* src, const uint8_t* type, const uint32_t* bb_links, float* rho, float* ux,
+                          float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane, int swap,
+                          hipStream_t s) {
   if (hi <= lo) return hipSuccess;
   const dim3 g(grid_for(hi - lo, 256));
-  if (swap) hipLaunchKernelGGL(k_moments<true>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
-  else hipLaunchKernelGGL(k_moments<false>, g, dim3(256), 0, s, src, type, rho, ux, uy, uz, lo, hi, pitch, plane);
+  if (swap)
+    hipLaunchKernelGGL(k_moments<true>, g, dim3(256), 0, s, src, type, bb_links, rho, ux, uy, uz, lo, hi, pitch, plane);
+  else
+    hipLaunchKernelGGL(k_moments<false>, g, dim3(256), 0, s, src, type, bb_links, rho, ux, uy, uz, lo, hi, pitch, plane);
   return hipGetLastError();
 }
 
-hipError_t launch_vel_terms(const float* src, const uint8_t* type, const int* ref_idx, float* terms, int64_t lo,
-                            int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
+hipError_t launch_vel_terms(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* ref_idx,
+                            float* terms, int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s) {
   if (hi <= lo) return hipSuccess;
   const dim3 g(grid_for(hi - lo, 256));
-  if (swap) hipLaunchKernelGGL(k_vel_terms<true>, g, dim3(256), 0, s, src, type, ref_idx, terms, lo, hi, pitch, plane);
-  else hipLaunchKernelGGL(k_vel_terms<false>, g, dim3(256), 0, s, src, type, ref_idx, terms, lo, hi, pitch, plane);
+  if (swap)
+    hipLaunchKernelGGL(k_vel_terms<true>, g, dim3(256), 0, s, src, type, bb_links, ref_idx, terms, lo, hi, pitch, plane);
+  else
+    hipLaunchKernelGGL(k_vel_terms<false>, g, dim3(256), 0, s, src, type, bb_links, ref_idx, terms, lo, hi, pitch,
+                       plane);
   return hipGetLastError();
 }
 

@@ -116,6 +116,12 @@ struct MainArgs {
   // at index (dy + 1) * 3 + dz + 1 (dy, dz in -1..1).
   const int4* rowrec;
   const int* group_row;  // the storage row of every group-list entry
+  int bb_pull;           // 1: bounce-back on the consumer side (one-cell compact ranges): a fluid
+                         // cell takes population q from its own slot opp(q) of the source buffer
+                         // where c - e_q is a wall -- the post-collision value the producer side
+                         // would have stored there -- and stores no wall slots
+  int bb_raw;            // this launch is the lattice's first step of a case whose walls do not
+                         // bounce back at step 0 (all but LDC): wall slots are pulled raw
   const int4* grouprec;  // one-cell compact ranges (no list): the row record of every compact
                          // 4-cell group (3 x int4, rowrec's layout); group_bc is then indexed by
                          // compact group
@@ -184,14 +190,16 @@ hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s
 // stay 0), then CUB's two-pass device-reduction tree over terms[0 .. n) -- pass 1: `grid`
 // blocks of 256 threads over tiles of 256 * ipt items (even share), pass 2: one block over the
 // partials, then the residual logic on S = 0.f + the tree's sum
-hipError_t launch_vel_terms(const float* src, const uint8_t* type, const int* ref_idx, float* terms, int64_t lo,
-                            int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
+hipError_t launch_vel_terms(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* ref_idx,
+                            float* terms, int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
 int cub_grid(int64_t n, int ipt, int grid_cap);
 hipError_t launch_cub_tree(const float* terms, int64_t n, int ipt, int vec, int grid_cap, float* partials,
                            ConvState* conv, float* hist_slot, hipStream_t s);
-// lazy macros: (rho, u) of the fluid cells in [lo, hi) from the last step's source buffer
-hipError_t launch_moments(const float* src, const uint8_t* type, float* rho, float* ux, float* uy, float* uz,
-                          int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
+// lazy macros: (rho, u) of the fluid cells in [lo, hi) from the last step's source buffer;
+// bb_links (nullable): the wall links of a consumer-side bounce-back step (MainArgs::bb_pull)
+hipError_t launch_moments(const float* src, const uint8_t* type, const uint32_t* bb_links, float* rho, float* ux,
+                          float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane, int swap,
+                          hipStream_t s);
 // per local plane digest of the fluid (rho, u) bits keyed by global coordinates (lbm_field_digest);
 // out[nz] must be zeroed
 hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux, const float* uy, const float* uz,

@@ -29,10 +29,11 @@ def vessel_mask(shape, seed, nballs=5):
 
 
 def stored_cells(geo):
-    """Cells whose populations are defined in every storage mode: fluid, walls and boundary
-    cells.  Compact rows (LBM_TUNE_COMPACT) keep no slots for the passive cells outside the row
-    spans, which lbm_get_f then reports as 0; lbm.h defines only the fluid cells' values."""
-    return (geo != 0) & (geo != -1)
+    """Cells whose populations agree in every storage mode: fluid and boundary (NEE) cells.
+    Compact rows (LBM_TUNE_COMPACT) keep no slots for the passive cells outside the row spans,
+    which lbm_get_f then reports as 0, and their one-cell path bounces back on the consumer side,
+    so it never writes wall slots; lbm.h defines only the fluid cells' values."""
+    return (geo != 0) & (geo != -1) & (geo != 1)
 
 
 def inlet_tables(shape, seed):
