@@ -187,7 +187,12 @@ typedef enum {
                                    reference's index_transform, Poiseulle.cu:257-271, per row); 1 the
                                    dense box; 2 compact rows whenever the range takes group lists
                                    (LBM_TUNE_GROUPS 2 included) */
-  LBM_TUNE_COUNT = 11
+  LBM_TUNE_BOX = 11,            /* the device-generated cavity (geo == NULL, LBM_CASE_LDC) with a
+                                   power-of-two row pitch and plane: 0 (default) the step kernels
+                                   compute cell types and wall links from coordinates, and its
+                                   one-cell single-domain range bounces back on the consumer side;
+                                   1 they load them like any lattice's */
+  LBM_TUNE_COUNT = 12
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

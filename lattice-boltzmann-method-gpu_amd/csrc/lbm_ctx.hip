@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -166,9 +166,16 @@ struct lbm_ctx {
   float *crho = nullptr, *cux = nullptr, *cuy = nullptr, *cuz = nullptr;
   // slots per population buffer past the leading guard (the part checkpoints hold)
   int64_t pop_floats() const { return (compact ? nchunk_c : L.nchunk) * kQ * kChunk; }
-  // bounce-back on the consumer side (MainArgs::bb_pull): one-cell compact ranges read a wall
-  // link's value from the cell's own opposite slot, so no step writes wall slots
-  bool bb_pull() const { return compact && whole.quarter; }
+  // the device-generated cavity with power-of-two pitch and plane: the chunk kernels compute
+  // types and links from coordinates (MainArgs::box)
+  bool box = false;
+  // bounce-back on the consumer side (MainArgs::bb_pull): one-cell compact ranges and the
+  // one-cell whole-domain range of the cavity read a wall link's value from the cell's own
+  // opposite slot, so no step writes wall slots (the RCCL slab sequence keeps the producer side:
+  // lbm_attach_rccl first writes the wall slots once, k_bb_prime)
+  bool bb_pull() const {
+    return whole.quarter && (compact || (box && d.nz_global == d.nz && !comm && !comm_failed));
+  }
   // step k's source buffer holds wall slots that must be pulled raw (MainArgs::bb_raw): the
   // first step of a case whose walls do not bounce back at step 0
   bool bb_raw(int k) const { return k == 0 && !bb_immediate; }
@@ -353,6 +360,13 @@ void fill_main_args(lbm_ctx* c, MainArgs& a, int srcbuf) {
   a.swap = c->L.swap;
   a.bc_uniform = c->bc_uniform ? 1 : 0;
   a.bc_const = c->bc_const;
+  if (c->box) {
+    a.box = 1;
+    a.box_nx = c->L.nx; a.box_ny = c->L.ny; a.box_nzg = c->d.nz_global; a.box_zoff = c->d.z_offset;
+    a.box_xshift = c->L.xshift;
+    a.box_pshift = __builtin_ctz((unsigned)c->L.pitch);
+    a.box_lshift = __builtin_ctzll((unsigned long long)c->L.plane);
+  }
 }
 
 // one step of a range from buffer srcbuf into srcbuf ^ 1
@@ -360,7 +374,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
               double* part = nullptr, int step = -1) {
   MainArgs a{};
   fill_main_args(c, a, srcbuf);
-  a.bb_pull = (c->compact && r.quarter) ? 1 : 0;
+  a.bb_pull = (&r == &c->whole && c->bb_pull()) ? 1 : 0;
   a.bb_raw = c->bb_raw(step) ? 1 : 0;
   a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
@@ -1037,7 +1051,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1102,6 +1116,11 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   L.nchunk = L.ncell / kChunk;
   L.guard = (L.plane + L.pitch + 8 + kChunk - 1) / kChunk + 1;
   c->n_box = (int64_t)d.nx * d.ny * d.nz;
+  {
+    auto pow2 = [](int64_t v) { return v > 0 && (v & (v - 1)) == 0; };
+    c->box = !d.geo && d.case_kind == LBM_CASE_LDC && !L.swap && pow2(L.pitch) && pow2(L.plane) &&
+             g_tune[LBM_TUNE_BOX] != 1;
+  }
   if (L.ncell >= (int64_t(1) << 31) - 2 * kChunk) {
     g_create_error = "slab too large for 32-bit cell ids (split it into more z-slabs)";
     delete c;
@@ -2291,6 +2310,14 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
     c->err = "lbm_attach_rccl: a lattice in compact rows is a single domain (create slabs with nz_global, or "
              "lbm_tune(LBM_TUNE_COMPACT, 1))";
     return LBM_ERR_STATE;
+  }
+  if (c->bb_pull() && c->steps_done > 0) {
+    // the steps so far bounced back on the consumer side and wrote no wall slots; the slab
+    // sequence's producer side reads them from the next step on: store them once from the
+    // current state, as its last step's producers would have
+    HIPCK(c, launch_bb_prime(c->buf[c->cur], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap,
+                             c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
   }
   NCCK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;

@@ -500,6 +500,50 @@ __device__ __forceinline__ void nee_store_all(const MainArgs& a, const A& ad, ui
   (nee_store_q<Qs, SW>(a, ad, nl, b0, b1, b2, b3, b4, src, r, ux, uy, uz, p), ...);
 }
 
+// ---- the device-generated cavity: types from coordinates (MainArgs::box) ------------------
+// ldc.cu:468-502: wall shell [1, n-2]^3, fluid [2, n-3]^3, lid (velocity NEE, -y face) on the
+// plane y = ny-2 over x, z in [1, n-2].  A fluid cell's neighbour c - e_q is a wall when it lies
+// on the shell (x' = 1 or nx-2, y' = 1, z' = 1 or nzg-2) and not on the lid plane; the lid
+// supplies the populations with e_y = -1 of the row y = ny-3.  Masks of the directions by the
+// sign of one component: the wall beyond x = 1 is pulled along e_x = +1, and so on.
+template <int C, int S>
+constexpr uint32_t dirs_with() {  // directions whose component C (0 x, 1 y, 2 z) equals S
+  uint32_t m = 0;
+  for (int q = 1; q < kQ; ++q)
+    if ((C == 0 ? kEx[q] : C == 1 ? kEy[q] : kEz[q]) == S) m |= 1u << q;
+  return m;
+}
+struct BoxCell {
+  uint8_t t;        // the type byte k_classify / k_flag_fluid give the cell
+  uint32_t links;   // wall links (fluid cells)
+  uint32_t nl;      // NEE links (fluid cells)
+};
+__device__ __forceinline__ BoxCell box_cell(const MainArgs& a, int64_t c) {
+  const int64_t u = c + a.box_xshift;
+  const int x = (int)(u & ((1 << a.box_pshift) - 1));
+  const int y = (int)((u >> a.box_pshift) & ((1 << (a.box_lshift - a.box_pshift)) - 1));
+  const int z = (int)(u >> a.box_lshift) - 1 + a.box_zoff;
+  const int nx = a.box_nx, ny = a.box_ny, nz = a.box_nzg;
+  BoxCell b{kPassive, 0u, 0u};
+  const bool shell = x >= 1 && x <= nx - 2 && y >= 1 && y <= ny - 2 && z >= 1 && z <= nz - 2;
+  if (!shell) return b;
+  if (y == ny - 2) {
+    b.t = make_nee(kFaceNY, false);
+  } else if (x >= 2 && x <= nx - 3 && y >= 2 && z >= 2 && z <= nz - 3) {
+    uint32_t m = (x == 2 ? dirs_with<0, 1>() : 0u) | (x == nx - 3 ? dirs_with<0, -1>() : 0u) |
+                 (y == 2 ? dirs_with<1, 1>() : 0u) | (z == 2 ? dirs_with<2, 1>() : 0u) |
+                 (z == nz - 3 ? dirs_with<2, -1>() : 0u);
+    const bool lid = y == ny - 3;
+    if (lid) m &= ~dirs_with<1, -1>();
+    b.links = m;
+    b.nl = lid ? dirs_with<1, -1>() : 0u;
+    b.t = (uint8_t)(kFluid | (m ? kWallAdj : 0) | (lid ? kNeeAdj : 0));
+  } else {
+    b.t = kWall;
+  }
+  return b;
+}
+
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
 //        branch) the exact division, counted in exact_waves.  Both paths cost 210-218 VGPRs
@@ -507,9 +551,12 @@ __device__ __forceinline__ void nee_store_all(const MainArgs& a, const A& ad, ui
 //        SIMD ran slower (profiles/r03_fast3_ab.log).
 //  COMPACT (with GROUPS): compact rows -- the group's row record goes out beside the list
 //        entry's type byte and link masks, then the pulls (Rows).
-template <bool FAST, bool SW, bool MASK, bool GROUPS = false, bool COMPACT = false>
+//  BOX (chunk lists of the device-generated cavity): type bytes and wall links from the cells'
+//        coordinates (box_cell), no loads.
+template <bool FAST, bool SW, bool MASK, bool GROUPS = false, bool COMPACT = false, bool BOX = false>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
   static_assert(GROUPS || !COMPACT, "compact rows run over group lists");
+  static_assert(!(BOX && (GROUPS || SW)), "the cavity runs over x-row chunk lists");
   double acc = 0.0;
   int64_t c;
   bool need, take_lo, take_hi;
@@ -549,13 +596,21 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     take_hi = lane == 63;
     pull4_all<SW>(v, a.src, cb, cb + kChunk, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
   }
-  const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
-  const unsigned t4 = need ? t4r : 0u;
-  // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
-  // so this dependent load hides behind the arithmetic)
   constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
   uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-  if constexpr (GROUPS) {
+  unsigned t4;
+  if constexpr (BOX) {
+    const BoxCell b0 = box_cell(a, c), b1 = box_cell(a, c + 1), b2 = box_cell(a, c + 2), b3 = box_cell(a, c + 3);
+    t4 = need ? (unsigned)b0.t | ((unsigned)b1.t << 8) | ((unsigned)b2.t << 16) | ((unsigned)b3.t << 24) : 0u;
+    m0 = b0.links; m1 = b1.links; m2 = b2.links; m3 = b3.links;
+  } else {
+    const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
+    t4 = need ? t4r : 0u;
+  }
+  // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
+  // so this dependent load hides behind the arithmetic)
+  if constexpr (BOX) {
+  } else if constexpr (GROUPS) {
     // compact lists are wall-heavy: the lane's four masks go out beside the type bytes (one
     // 16-B load, no dependent round trip)
     const uint4 lk = *reinterpret_cast<const uint4*>(a.links + (need ? c : 0));
@@ -827,17 +882,40 @@ __device__ __forceinline__ double collide_cell1(const MainArgs& a, int64_t c, co
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
-template <bool SW>
+// the pulls of pull1w_all with consumer-side bounce-back (MainArgs::bb_pull): where bit q of wl
+// is set, population q comes from the cell's own slot opp(q)
+template <bool SW, int... Qs>
+__device__ __forceinline__ void pull1w_bb(float* f, const float* __restrict__ src, int64_t ch, int l, int pitch,
+                                          int64_t plane, uint32_t wl, std::integer_sequence<int, Qs...>) {
+  const int W = (int)((plane + pitch + 1) >> 8) + 2;
+  const float* base = src + (ch - W) * (kQ * kChunk);
+  const int r0 = l + W * kChunk;
+  ((f[Qs] = __builtin_nontemporal_load(
+        base + ((wl >> Qs) & 1u ? rel_aidx(r0, Dir<Qs>::opp) : rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs)))),
+   ...);
+}
+
+//  BOX: the device-generated cavity -- type byte and link masks from the coordinates, and (the
+//        whole domain, bb_pull) bounce-back on the consumer side: the pulls of wall links read
+//        the cell's own opposite slots, known before the first load
+template <bool SW, bool BOX = false>
 __device__ __forceinline__ double process_cell1(const MainArgs& a, int64_t ch, int l) {
   // the pulls go out with the type byte (one round trip; the guard chunks keep every
   // address of a lane that turns out to be idle inside the buffer)
   const int64_t c = ch * kChunk + l;
-  const uint8_t t = a.type[c];
-  const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
-  const uint32_t nl = a.nlinks[c];
   float f[kQ];
-  pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
-  return collide_cell1<SW, false>(a, c, AddrD{c, a.pitch, a.plane}, t, links, nl, f);
+  if constexpr (BOX) {
+    const BoxCell b = box_cell(a, c);
+    const bool pull_own = a.bb_pull && !a.bb_raw;
+    pull1w_bb<SW>(f, a.src, ch, l, a.pitch, a.plane, pull_own ? b.links : 0u, AllQ{});
+    return collide_cell1<SW, false>(a, c, AddrD{c, a.pitch, a.plane}, b.t, a.bb_pull ? 0u : b.links, b.nl, f);
+  } else {
+    const uint8_t t = a.type[c];
+    const uint32_t links = a.links[c];  // unconditionally: no dependent round trip on t
+    const uint32_t nl = a.nlinks[c];
+    pull1w_all<SW>(f, a.src, ch, l, a.pitch, a.plane, AllQ{});
+    return collide_cell1<SW, false>(a, c, AddrD{c, a.pitch, a.plane}, t, links, nl, f);
+  }
 }
 
 // One cell per lane over a compact group list (sparse one-cell ranges): wave w takes the 16
@@ -979,7 +1057,7 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
 }
 
 template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false, bool GROUPS = false,
-          bool COMPACT = false>
+          bool COMPACT = false, bool BOX = false>
 __device__ __forceinline__ void step_body(const MainArgs& a) {
   __shared__ double red[kBlock / 64];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -1028,7 +1106,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true, COMPACT>(a, (int64_t)idx * 64, lane, 0);
     } else if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
-        acc = process_cell1<SW>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
+        acc = process_cell1<SW, BOX>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
     } else if constexpr (STRIDE) {  // grid-stride: XCD (b & 7) takes its eighth of the list in order
       const int per = (a.nchunks + 7) >> 3;
       const int lo = (b & 7) * per, hi = min(a.nchunks, lo + per);
@@ -1039,7 +1117,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
       }
     } else if (idx < a.nchunks) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
-      acc = process_chunk<FAST, SW, MASK>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base
+      acc = process_chunk<FAST, SW, MASK, false, false, BOX>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base
     }
     slot += a.red_blocks + a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
@@ -1057,14 +1135,15 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
 // 4 cells per lane (big lattices): two waves per SIMD (210-253 VGPRs; one exact-division-only
 // instance runs one); MASK: the range has lane masks (sparse chunk lists); COMPACT: compact
 // rows (group lists only)
-template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false, bool COMPACT = false>
+template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false, bool COMPACT = false,
+          bool BOX = false>
 __global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
-  step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT>(a);
+  step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT, BOX>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
-template <bool SW, bool GROUPS = false, bool STRIDE = false, bool COMPACT = false>
+template <bool SW, bool GROUPS = false, bool STRIDE = false, bool COMPACT = false, bool BOX = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_step1(const MainArgs a) {
-  step_body<false, true, SW, false, STRIDE, GROUPS, COMPACT>(a);
+  step_body<false, true, SW, false, STRIDE, GROUPS, COMPACT, BOX>(a);
 }
 
 // ---- residual --------------------------------------------------------------------------
@@ -1702,7 +1781,13 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   const bool sw = a.swap != 0;
   Kern k;
   const size_t lds = 0;
-  if (a.rowrec) {  // compact rows: one cell per lane without a list, or 4-cell group lists
+  if (a.box && !a.swap && !a.groups && !a.chunk_stride) {  // the device-generated cavity
+    if (a.quarter) k = k_step1<false, false, false, false, true>;
+    else if (a.fast_div) k = a.lane_masks ? k_step<true, false, true, false, false, false, true>
+                                          : k_step<true, false, false, false, false, false, true>;
+    else k = a.lane_masks ? k_step<false, false, true, false, false, false, true>
+                          : k_step<false, false, false, false, false, false, true>;
+  } else if (a.rowrec) {  // compact rows: one cell per lane without a list, or 4-cell group lists
     if (a.quarter) {
       if (!a.grouprec) return hipErrorInvalidValue;
       k = sw ? k_step1<true, false, false, true> : k_step1<false, false, false, true>;

@@ -116,6 +116,13 @@ struct MainArgs {
   // at index (dy + 1) * 3 + dz + 1 (dy, dz in -1..1).
   const int4* rowrec;
   const int* group_row;  // the storage row of every group-list entry
+  // The device-generated cavity (box = 1; ldc.cu:468-502 on global coordinates, lbm_desc.geo
+  // NULL, power-of-two pitch and plane): class, wall links and NEE links of every cell follow
+  // from its coordinates, so the step kernels compute them instead of loading the type bytes
+  // and link masks.  Cell c sits at s0 = (c + xshift) & (pitch - 1), s1 = bits above, storage
+  // plane zs = (c + xshift) >> box_lshift, global z = zs - 1 + z_offset.
+  int box;
+  int box_nx, box_ny, box_nzg, box_zoff, box_xshift, box_pshift, box_lshift;
   int bb_pull;           // 1: bounce-back on the consumer side (one-cell compact ranges): a fluid
                          // cell takes population q from its own slot opp(q) of the source buffer
                          // where c - e_q is a wall -- the post-collision value the producer side
