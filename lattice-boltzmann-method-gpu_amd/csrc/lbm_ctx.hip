@@ -169,12 +169,12 @@ struct lbm_ctx {
   // the device-generated cavity with power-of-two pitch and plane: the chunk kernels compute
   // types and links from coordinates (MainArgs::box)
   bool box = false;
-  // bounce-back on the consumer side (MainArgs::bb_pull): one-cell compact ranges and the
-  // one-cell whole-domain range of the cavity read a wall link's value from the cell's own
-  // opposite slot, so no step writes wall slots (the RCCL slab sequence keeps the producer side:
+  // bounce-back on the consumer side (MainArgs::bb_pull): compact ranges and the one-cell
+  // whole-domain range of the cavity read a wall link's value from the cell's own opposite
+  // slot, so no step writes wall slots (the RCCL slab sequence keeps the producer side:
   // lbm_attach_rccl first writes the wall slots once, k_bb_prime)
   bool bb_pull() const {
-    return whole.quarter && (compact || (box && d.nz_global == d.nz && !comm && !comm_failed));
+    return compact || (whole.quarter && box && d.nz_global == d.nz && !comm && !comm_failed);
   }
   // step k's source buffer holds wall slots that must be pulled raw (MainArgs::bb_raw): the
   // first step of a case whose walls do not bounce back at step 0

@@ -41,6 +41,8 @@ namespace lbm {
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -238,6 +240,63 @@ __device__ __forceinline__ void pull4_g(f4* v, const float* __restrict__ src, co
   float e[kQ];
   ((pull_issue_g<Qs, SW>(v[Qs], e[Qs], src, ad, need)), ...);
   ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], take_lo, take_hi)), ...);
+}
+template <bool SW, class A, int... Qs>
+__device__ __forceinline__ void pull4_g_issue(f4* v, float* e, const float* __restrict__ src, const A& ad, bool need,
+                                              std::integer_sequence<int, Qs...>) {
+  ((pull_issue_g<Qs, SW>(v[Qs], e[Qs], src, ad, need)), ...);
+}
+template <bool SW, int... Qs>
+__device__ __forceinline__ void pull4_compose(f4* v, const float* e, bool take_lo, bool take_hi,
+                                              std::integer_sequence<int, Qs...>) {
+  ((v[Qs] = pull_compose<Qs, SW>(v[Qs], e[Qs], take_lo, take_hi)), ...);
+}
+
+// Bounce-back on the consumer side for 4-cell lanes (MainArgs::bb_pull, compact rows): a cell
+// whose neighbour c - e_q is a wall takes population q from its own slot opp(q) of the source
+// buffer -- the post-collision value the producer side would have stored into the wall (the
+// reference's d_dst[q][W] = d_dst[opp q][W + e_q], Poiseulle.cu:601-746, read where it was
+// written).  For every direction that some lane of the wave links, the linking lanes' own 16-B
+// slices of slot opp(q) go to the wave's LDS by DMA (global_load_lds: nothing in VGPRs while in
+// flight), issued beside the pulls; once in, each cell with the link takes its value.  No wall
+// slot is ever written, so lanes sharing their 4-cell group with walls store whole vectors.
+struct OwnLds {
+  f4 s[kQ][64];  // per direction q: the wave's own slices of slot opp(q)
+};
+template <int Q>
+__device__ __forceinline__ void bb_own_issue(const float* __restrict__ src, int c, uint32_t lm, OwnLds& L) {
+  if constexpr (Q > 0) {
+    const bool mine = (lm >> Q) & 1u;
+    if (__any(mine)) {  // wave-uniform
+      if (mine)
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + fidx(c, Dir<Q>::opp)), (lds_ptr_t)&L.s[Q][0], 16, 0, 2);
+    }
+  }
+}
+template <int Q>
+__device__ __forceinline__ void bb_own_merge(f4* v, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3, uint32_t lm,
+                                             int lane, const OwnLds& L) {
+  if constexpr (Q > 0) {
+    const bool mine = (lm >> Q) & 1u;
+    if (__any(mine)) {
+      if (mine) {
+        const f4 o = L.s[Q][lane];
+        v[Q] = f4{(m0 >> Q) & 1u ? o.x : v[Q].x, (m1 >> Q) & 1u ? o.y : v[Q].y, (m2 >> Q) & 1u ? o.z : v[Q].z,
+                  (m3 >> Q) & 1u ? o.w : v[Q].w};
+      }
+    }
+  }
+}
+template <int... Qs>
+__device__ __forceinline__ void bb_own_issue_all(const float* __restrict__ src, int c, uint32_t lm, OwnLds& L,
+                                                 std::integer_sequence<int, Qs...>) {
+  (bb_own_issue<Qs>(src, c, lm, L), ...);
+}
+template <int... Qs>
+__device__ __forceinline__ void bb_own_merge_all(f4* v, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                                 uint32_t lm, int lane, const OwnLds& L,
+                                                 std::integer_sequence<int, Qs...>) {
+  (bb_own_merge<Qs>(v, m0, m1, m2, m3, lm, lane, L), ...);
 }
 
 template <int J, int... Qs>
@@ -562,6 +621,12 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   bool need, take_lo, take_hi;
   f4 v[kQ];
   RowsRef ad{};  // COMPACT: the lane's cell and row (Rows again for the bounce-back stores)
+  constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
+  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+  unsigned t4 = 0u;
+  // COMPACT: bounce-back on the consumer side (bb_own_*); step 0 of a case whose walls do not
+  // bounce back yet pulls the walls raw
+  const bool consumer = COMPACT && a.bb_pull && !a.bb_raw;
   if constexpr (GROUPS) {
     // compact groups: lane = one 4-cell group of the range's list (cb: the wave's first entry);
     // a lane takes its x-neighbours' cells from the neighbouring lane when that lane holds the
@@ -581,8 +646,29 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     take_hi = lane == 63 || gn != g + 4;
     c = g;
     if constexpr (COMPACT) {
+      // type bytes and link masks beside the row record (one round trip), then the pulls and,
+      // for the wall links, the own slices (consumer-side bounce-back) -- one more round trip
       const int row = a.group_row[gs];
-      pull4_g<SW>(v, a.src, Rows::load(a.rowrec, c, row), take_lo, take_hi, need, AllQ{});
+      t4 = need ? *reinterpret_cast<const unsigned*>(a.type + c) : 0u;
+      const uint4 lk = *reinterpret_cast<const uint4*>(a.links + (need ? c : 0));
+      float e[kQ];
+      pull4_g_issue<SW>(v, e, a.src, Rows::load(a.rowrec, c, row), need, AllQ{});
+      m0 = (t4 & (kWallAdj << 0)) ? lk.x : 0u;
+      m1 = (t4 & (kWallAdj << 8)) ? lk.y : 0u;
+      m2 = (t4 & (kWallAdj << 16)) ? lk.z : 0u;
+      m3 = (t4 & (kWallAdj << 24)) ? lk.w : 0u;
+      if (consumer) {
+        __shared__ OwnLds own_lds[kBlock / 64];
+        OwnLds& L = own_lds[threadIdx.x >> 6];
+        const uint32_t lm = m0 | m1 | m2 | m3;
+        bb_own_issue_all(a.src, (int)c, lm, L, AllQ{});
+        pull4_compose<SW>(v, e, take_lo, take_hi, AllQ{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes are in
+        bb_own_merge_all(v, m0, m1, m2, m3, lm, lane, L, AllQ{});
+        m0 = m1 = m2 = m3 = 0u;  // no wall stores
+      } else {
+        pull4_compose<SW>(v, e, take_lo, take_hi, AllQ{});
+      }
       ad = RowsRef{a.rowrec, c, row};
     } else {
       pull4_all<SW>(v, a.src, c, c + 4, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
@@ -596,20 +682,17 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     take_hi = lane == 63;
     pull4_all<SW>(v, a.src, cb, cb + kChunk, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
   }
-  constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
-  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-  unsigned t4;
   if constexpr (BOX) {
     const BoxCell b0 = box_cell(a, c), b1 = box_cell(a, c + 1), b2 = box_cell(a, c + 2), b3 = box_cell(a, c + 3);
     t4 = need ? (unsigned)b0.t | ((unsigned)b1.t << 8) | ((unsigned)b2.t << 16) | ((unsigned)b3.t << 24) : 0u;
     m0 = b0.links; m1 = b1.links; m2 = b2.links; m3 = b3.links;
-  } else {
+  } else if constexpr (!COMPACT) {
     const unsigned t4r = *reinterpret_cast<const unsigned*>(a.type + (need ? c : 0));
     t4 = need ? t4r : 0u;
   }
   // wall-link masks of the lane's wall-adjacent cells (consumed only after the collision,
   // so this dependent load hides behind the arithmetic)
-  if constexpr (BOX) {
+  if constexpr (BOX || COMPACT) {
   } else if constexpr (GROUPS) {
     // compact lists are wall-heavy: the lane's four masks go out beside the type bytes (one
     // 16-B load, no dependent round trip)
@@ -666,7 +749,8 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   // of the step before the xshift alignment), and a wave with one such lane issues both store
   // paths (4 x 19 + 19 instructions: every y-row wave of the C3 pipe, before nee_chunks).
   const unsigned lo4 = t4 & 0x01010101u, hi4 = (t4 >> 1) & 0x01010101u;
-  const unsigned special = (lo4 ^ hi4) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);  // wall, NEE, pulled passive
+  // wall (unless bounce-back is on the consumer side: no wall slot is ever read), NEE, pulled passive
+  const unsigned special = (consumer ? (hi4 & ~lo4) : (lo4 ^ hi4)) | (~(lo4 | hi4) & (t4 >> 2) & 0x01010101u);
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
   const bool keep_others = special != 0u || !lane_in || (!a.nee_chunks && (t4 & kNee4));
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
@@ -685,7 +769,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     if constexpr (COMPACT) return ad.get();
     else return AddrD{c, a.pitch, a.plane};
   }();
-  if (__any(t4 & kWall4)) {  // wave-uniform: whole-group bounce-back stores (bb_group_one)
+  if (!consumer && __any(t4 & kWall4)) {  // wave-uniform: whole-group bounce-back stores (bb_group_one)
     const uint32_t b0 = (store & 1u) ? m0 : 0u, b1 = (store & 2u) ? m1 : 0u, b2 = (store & 4u) ? m2 : 0u,
                    b3 = (store & 8u) ? m3 : 0u;
     const uint32_t nb0 = take_hi ? 0u : u_from_next(b0), pb3 = take_lo ? 0u : u_from_prev(b3);
@@ -698,7 +782,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     const uint32_t g = g0 | gp | gm;
     m0 &= ~(g0 | gm | gpp); m1 &= ~g; m2 &= ~g; m3 &= ~(g0 | gp | gmn);
   }
-  if (t4 & kWall4) {  // rare, divergent: lanes holding wall-adjacent cells
+  if (!consumer && (t4 & kWall4)) {  // rare, divergent: lanes holding wall-adjacent cells
     if (store & 1u) bb_store_cell<0, SW>(a.dst, bad, m0, v);
     if (store & 2u) bb_store_cell<1, SW>(a.dst, bad, m1, v);
     if (store & 4u) bb_store_cell<2, SW>(a.dst, bad, m2, v);
@@ -1006,13 +1090,15 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const float4* r = a.nee_bc + (int64_t)i * kNeeSlots;
   const BcSlots bc = a.bc_uniform ? BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const}
                                   : BcSlots{r[0], r[1], r[2], r[3], r[4]};
-  const uint32_t links = a.nee_chunks ? 0u : a.links[c];
+  // consumer-side bounce-back (compact rows): the wall links select the cell's own slots
+  const bool consumer = COMPACT && a.bb_pull && !a.bb_raw;
+  const uint32_t links = (a.nee_chunks && !consumer) ? 0u : a.links[c];
   float f[kQ];
   using A = std::conditional_t<COMPACT, RowsRef, AddrD>;
   A ad;
   if constexpr (COMPACT) {
     const int row = a.cell_row[i];
-    pull1_addr<SW>(f, a.src, Rows::load(a.rowrec, c, row), AllQ{});
+    pull1_bb<SW>(f, a.src, Rows::load(a.rowrec, c, row), (int)c, consumer ? links : 0u, AllQ{});
     ad = RowsRef{a.rowrec, c, row};
   } else {
     ad = AddrD{c, a.pitch, a.plane};
@@ -1027,7 +1113,7 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   const Pref pre = relax1(f, a, rho, ux, uy, uz);
   nee_store_all<SW>(a, ad.get(), nl, bc, Post1{f}, rho, ux, uy, uz, pre, AllQ{});
   if (a.nee_chunks) return 0.0;  // the chunk wave stores the cell and sums its |u|
-  fix_store_all<SW>(f, a.dst, c, ad, links, AllQ{});
+  fix_store_all<SW>(f, a.dst, c, ad, a.bb_pull ? 0u : links, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
@@ -1137,7 +1223,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
 // rows (group lists only)
 template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false, bool COMPACT = false,
           bool BOX = false>
-__global__ __launch_bounds__(kBlock) void k_step(const MainArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(const MainArgs a) {
   step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT, BOX>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
@@ -1887,8 +1973,6 @@ __global__ __launch_bounds__(256) void k_probe_tiles(const f4* __restrict__ a, f
 // The same tiles moved by LDS-DMA (global_load_lds, 16 B per lane: the loads take no VGPRs, so
 // a wave keeps its whole 16-KB tile in flight in LDS; two 64-KB workgroups per CU), then
 // ds_read_b128 + stores; NT: the loads' non-temporal policy (MI355X_MICROARCH.md, ldsdma-fill)
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 template <bool NT>
 __global__ __launch_bounds__(256) void k_probe_lds(const f4* __restrict__ a, f4* __restrict__ b, int64_t ntiles) {
   __shared__ f4 tile[4][1024];
