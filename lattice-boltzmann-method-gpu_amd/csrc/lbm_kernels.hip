@@ -263,8 +263,8 @@ __device__ __forceinline__ void pull4_compose(f4* v, const float* e, bool take_l
 struct OwnLds {
   f4 s[kQ][64];  // per direction q: the wave's own slices of slot opp(q)
 };
-template <int Q>
-__device__ __forceinline__ void bb_own_issue(const float* __restrict__ src, int c, uint32_t lm, OwnLds& L) {
+template <int Q, class CT>
+__device__ __forceinline__ void bb_own_issue(const float* __restrict__ src, CT c, uint32_t lm, OwnLds& L) {
   if constexpr (Q > 0) {
     const bool mine = (lm >> Q) & 1u;
     if (__any(mine)) {  // wave-uniform
@@ -287,8 +287,8 @@ __device__ __forceinline__ void bb_own_merge(f4* v, uint32_t m0, uint32_t m1, ui
     }
   }
 }
-template <int... Qs>
-__device__ __forceinline__ void bb_own_issue_all(const float* __restrict__ src, int c, uint32_t lm, OwnLds& L,
+template <class CT, int... Qs>
+__device__ __forceinline__ void bb_own_issue_all(const float* __restrict__ src, CT c, uint32_t lm, OwnLds& L,
                                                  std::integer_sequence<int, Qs...>) {
   (bb_own_issue<Qs>(src, c, lm, L), ...);
 }
@@ -661,10 +661,13 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
         __shared__ OwnLds own_lds[kBlock / 64];
         OwnLds& L = own_lds[threadIdx.x >> 6];
         const uint32_t lm = m0 | m1 | m2 | m3;
-        bb_own_issue_all(a.src, (int)c, lm, L, AllQ{});
+        const bool walls = __any(lm != 0u);  // wave-uniform
+        if (walls) bb_own_issue_all(a.src, (int)c, lm, L, AllQ{});
         pull4_compose<SW>(v, e, take_lo, take_hi, AllQ{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes are in
-        bb_own_merge_all(v, m0, m1, m2, m3, lm, lane, L, AllQ{});
+        if (walls) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes are in
+          bb_own_merge_all(v, m0, m1, m2, m3, lm, lane, L, AllQ{});
+        }
         m0 = m1 = m2 = m3 = 0u;  // no wall stores
       } else {
         pull4_compose<SW>(v, e, take_lo, take_hi, AllQ{});
@@ -905,8 +908,8 @@ __device__ __forceinline__ void pull1_addr(float* f, const float* __restrict__ s
 // the same with bounce-back on the consumer side (MainArgs::bb_pull): where bit q of wl is set
 // (c - e_q a wall), population q comes from the cell's own slot opp(q) -- Poiseulle.cu:601-746's
 // d_dst[q][W] = d_dst[opp q][W + e_q] with W + e_q = c, read where it was stored
-template <bool SW, class A, int... Qs>
-__device__ __forceinline__ void pull1_bb(float* f, const float* __restrict__ src, const A& ad, int c, uint32_t wl,
+template <bool SW, class A, class CT, int... Qs>
+__device__ __forceinline__ void pull1_bb(float* f, const float* __restrict__ src, const A& ad, CT c, uint32_t wl,
                                          std::integer_sequence<int, Qs...>) {
   ((f[Qs] = __builtin_nontemporal_load(
         src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp) : fidx(ad.template nb<Qs, SW>(), Qs)))),
