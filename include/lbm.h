@@ -154,7 +154,11 @@ const char* lbm_last_error(const lbm_ctx* ctx); /* NULL ctx: last creation error
  * value, or LBM_ERR_ARG for an unknown knob / value.  Fields (populations, rho, u) are
  * bit-identical for every setting; the residual's fp64 |u| sum is accumulated per launch block,
  * so launch-shape knobs (CELLS_PER_LANE, GRID_STRIDE, FUSED_RESIDUAL) can change its last bits
- * and with them, rarely, the step a convergence-controlled run stops at. */
+ * and with them, rarely, the step a convergence-controlled run stops at.  The default shape also
+ * follows the device's CU count (grid-stride block counts) and the lattice's sparsity, so that
+ * stop step is reproducible run to run on one GPU model, not across models.  A stop step that
+ * must not depend on the device: lbm_set_residual_order(LBM_SUM_CUB_TREE, ...), whose terms are
+ * summed in storage order by a fixed tree, whatever the launch shape. */
 typedef enum {
   LBM_TUNE_ROW_AXIS = 0,        /* stands in for lbm_desc.row_axis = 0: 0 choose, 1 x, 2 y */
   LBM_TUNE_CELLS_PER_LANE = 1,  /* step kernel: 0 by size, 1 one cell per lane, 4 four */
