@@ -625,7 +625,8 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     // (lo & ~63) + 64 w (process_compact_cell1); the boundary records of the NEE-adjacent cells
     // by compact group (group_bc), gathered from the dense arrays
     const int64_t base = lo & ~int64_t(63), waves = (hi - base + 63) / 64;
-    r.main_blocks = waves ? (int)std::max<int64_t>(8, ((waves + kBlock / 64 - 1) / (kBlock / 64) + 7) / 8 * 8) : 0;
+    constexpr int wpb = kBlock1c / 64;  // k_step1c's workgroups
+    r.main_blocks = waves ? (int)std::max<int64_t>(8, ((waves + wpb - 1) / wpb + 7) / 8 * 8) : 0;
     int64_t fl = 0;
     for (int64_t k = lo; k < hi; ++k) fl += (t[k] & kClassMask) == kFluid;
     r.group_fill = hi > base ? (double)fl / (double)(64 * waves) : 1.0;

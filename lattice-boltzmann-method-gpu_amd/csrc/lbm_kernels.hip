@@ -1146,9 +1146,9 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
 }
 
 template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false, bool GROUPS = false,
-          bool COMPACT = false, bool BOX = false>
-__device__ __forceinline__ void step_body(const MainArgs& a) {
-  __shared__ double red[kBlock / 64];
+          bool COMPACT = false, bool BOX = false, int WPB = kBlock / 64>
+__device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefronts per workgroup
+  __shared__ double red[WPB];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
   double acc = 0.0;
   int slot;
@@ -1157,7 +1157,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     slot = blockIdx.x;
     if (blockIdx.x == 0 && a.red_partial != nullptr) {
       double t = 0.0;
-      for (int i = threadIdx.x; i < a.red_n; i += kBlock) t += a.red_partial[i];  // fixed order
+      for (int i = threadIdx.x; i < a.red_n; i += WPB * 64) t += a.red_partial[i];  // fixed order
       t = block_sum(t, red);
       if (threadIdx.x == 0) {
         a.red_conv->s_local = t;
@@ -1173,23 +1173,23 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     // chunks and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
     const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
     slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
-    const int idx = slot * (kBlock / 64) + wave;
+    const int idx = slot * (WPB) + wave;
     if constexpr (QUARTER && COMPACT) {  // one cell per lane over compact rows, no list
       acc = process_compact_cell1<SW>(a, idx, lane);
     } else if constexpr (QUARTER && GROUPS && STRIDE) {  // the same, grid-stride over XCD (b & 7)'s eighth
       const int64_t nw = (a.ngroups + 15) >> 4;
       const int64_t per = (nw + 7) >> 3;
       const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
-      const int step = (a.main_blocks >> 3) * (kBlock / 64);
-      for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step) acc += process_group_cell1<SW, COMPACT>(a, i, lane);
+      const int step = (a.main_blocks >> 3) * (WPB);
+      for (int64_t i = lo + (b >> 3) * (WPB) + wave; i < hi; i += step) acc += process_group_cell1<SW, COMPACT>(a, i, lane);
     } else if constexpr (QUARTER && GROUPS) {  // one cell per lane over the compact group list
       if ((int64_t)idx * 16 < a.ngroups) acc = process_group_cell1<SW, COMPACT>(a, idx, lane);
     } else if constexpr (GROUPS && STRIDE) {  // compact groups, grid-stride over XCD (b & 7)'s eighth of the list
       const int64_t nw = (a.ngroups + 63) >> 6;  // 64-entry wave loads
       const int64_t per = (nw + 7) >> 3;
       const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
-      const int step = (a.main_blocks >> 3) * (kBlock / 64);
-      for (int64_t i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step)
+      const int step = (a.main_blocks >> 3) * (WPB);
+      for (int64_t i = lo + (b >> 3) * (WPB) + wave; i < hi; i += step)
         acc += process_chunk<FAST, SW, false, true, COMPACT>(a, i * 64, lane, 0);
     } else if constexpr (GROUPS) {  // compact 4-cell groups: wave idx takes list entries 64 idx ..
       if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true, COMPACT>(a, (int64_t)idx * 64, lane, 0);
@@ -1199,8 +1199,8 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {
     } else if constexpr (STRIDE) {  // grid-stride: XCD (b & 7) takes its eighth of the list in order
       const int per = (a.nchunks + 7) >> 3;
       const int lo = (b & 7) * per, hi = min(a.nchunks, lo + per);
-      const int step = (a.main_blocks >> 3) * (kBlock / 64);
-      for (int i = lo + (b >> 3) * (kBlock / 64) + wave; i < hi; i += step) {
+      const int step = (a.main_blocks >> 3) * (WPB);
+      for (int i = lo + (b >> 3) * (WPB) + wave; i < hi; i += step) {
         const uint64_t lm = MASK ? a.lane_masks[i] : ~0ull;
         acc += process_chunk<FAST, SW, MASK>(a, chunk_of(a, i) * kChunk, lane, lm);
       }
@@ -1233,6 +1233,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
 template <bool SW, bool GROUPS = false, bool STRIDE = false, bool COMPACT = false, bool BOX = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_step1(const MainArgs a) {
   step_body<false, true, SW, false, STRIDE, GROUPS, COMPACT, BOX>(a);
+}
+// one cell per lane over compact rows without a list (vessel trees), two waves per workgroup
+template <bool SW>
+__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(4))) void k_step1c(const MainArgs a) {
+  step_body<false, true, SW, false, false, false, true, false, kBlock1c / 64>(a);
 }
 
 // ---- residual --------------------------------------------------------------------------
@@ -1879,7 +1884,7 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   } else if (a.rowrec) {  // compact rows: one cell per lane without a list, or 4-cell group lists
     if (a.quarter) {
       if (!a.grouprec) return hipErrorInvalidValue;
-      k = sw ? k_step1<true, false, false, true> : k_step1<false, false, false, true>;
+      k = sw ? k_step1c<true> : k_step1c<false>;
     } else if (!a.groups) {
       return hipErrorInvalidValue;
     } else if (a.chunk_stride) {
@@ -1910,7 +1915,8 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
     else if (a.lane_masks) k = sw ? k_step<false, true, true> : k_step<false, false, true>;
     else k = sw ? k_step<false, true, false> : k_step<false, false, false>;
   }
-  hipLaunchKernelGGL(k, grid, dim3(kBlock), lds, s, a);
+  const bool c1 = !(a.box && !a.swap && !a.groups && !a.chunk_stride) && a.rowrec && a.quarter;
+  hipLaunchKernelGGL(k, grid, dim3(c1 ? kBlock1c : kBlock), lds, s, a);
   return hipGetLastError();
 }
 

@@ -16,6 +16,10 @@ namespace lbm {
 constexpr int kChunk = 256;
 constexpr int kQ = 19;
 constexpr int kBlock = 256;  // 4 wavefronts, one chunk each
+// the one-cell kernel over compact rows (vessel trees): 2 wavefronts per workgroup, so that a
+// few thousand waves spread evenly over the CUs (interleaved A/B: C4 8.74 -> 8.46 us, coronary
+// 37.5 -> 36.0 us; one-wave workgroups halve its residency, profiles/r04_workgroup_size_ab.log)
+constexpr int kBlock1c = 128;
 
 __host__ __device__ __forceinline__ int64_t aidx(int64_t c, int q) {
   return ((c >> 8) * kQ + q) * kChunk + (c & (kChunk - 1));
