@@ -62,6 +62,11 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
   bool nee_chunks = false;  // 4-cell ranges: chunk waves also store the NEE-adjacent cells (MainArgs)
+  // one-cell ranges whose waves all fit on the device at once: the fused residual's blocks go
+  // last (MainArgs::red_last), so that no chunk wave waits for a slot behind them (LDC 64^3
+  // 11.30 -> 11.14 us, C4 8.48 -> 8.27 us; a grid of several rounds -- the coronary tree 36.0 ->
+  // 39.6 us -- would wait for the residual at its end instead; profiles/r04_red_last_ab.log)
+  bool one_round = false;
   int* groups = nullptr;  // sparse ranges: compact list of active 4-cell groups (both paths)
   int64_t ngroups = 0;
   int* group_bc = nullptr;         // one-cell group lists: per entry, its NEE records' index or -1
@@ -396,6 +401,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   if (fr) {
     a.partial = fr->part;
     a.red_blocks = 8;
+    a.red_last = r.one_round ? 1 : 0;
     a.red_partial = fr->prev;
     a.red_n = c->red_n;
     a.red_conv = c->conv;
@@ -749,6 +755,13 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       r.main_blocks = cap;
       r.stride = true;
     }
+  }
+  if (r.quarter) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->d.device) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int64_t waves = (int64_t)r.main_blocks * ((cv ? kBlock1c : kBlock) / 64);  // four per SIMD fit
+    r.one_round = waves <= (int64_t)cus * 16;
   }
   r.nee_waves = nee_waves_for(r.n_nee, contig);
   r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);

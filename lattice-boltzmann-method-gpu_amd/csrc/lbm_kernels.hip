@@ -1152,10 +1152,14 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
   double acc = 0.0;
   int slot;
-  const int bx = (int)blockIdx.x - a.red_blocks;
-  if (bx < 0) {  // leading reduction group: block 0 finishes the previous step
-    slot = blockIdx.x;
-    if (blockIdx.x == 0 && a.red_partial != nullptr) {
+  // the reduction group leads the grid, or trails it (red_last: a grid of one round of waves,
+  // whose chunk waves then all start at once)
+  const int nwork = a.nee_blocks + a.main_blocks;
+  const int bx = a.red_last ? ((int)blockIdx.x < nwork ? (int)blockIdx.x : -1) : (int)blockIdx.x - a.red_blocks;
+  const int rb = a.red_last ? (int)blockIdx.x - nwork : (int)blockIdx.x;
+  if (bx < 0) {  // reduction group: its first block finishes the previous step
+    slot = rb;
+    if (rb == 0 && a.red_partial != nullptr) {
       double t = 0.0;
       for (int i = threadIdx.x; i < a.red_n; i += WPB * 64) t += a.red_partial[i];  // fixed order
       t = block_sum(t, red);
@@ -1210,7 +1214,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
     }
     slot += a.red_blocks + a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
-    slot = blockIdx.x;
+    slot = a.red_blocks + bx;
     if constexpr (!QUARTER) {  // one-cell ranges have no NEE blocks
       const int w = (int)threadIdx.x >> 6;
       const int i = (bx * a.nee_waves + w) * 64 + ((int)threadIdx.x & 63);
