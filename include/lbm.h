@@ -263,7 +263,9 @@ int lbm_get_macros(lbm_ctx* ctx, float* rho, float* ux, float* uy, float* uz);
  * a size-independent check at lattice sizes whose fields are too large to copy to the host. */
 int lbm_field_digest(lbm_ctx* ctx, uint64_t* plane_digest);
 /* Populations of the last step (the next step's source), SoA [19][nz][ny][nx]; only fluid
- * cells carry reference-defined values. */
+ * cells carry reference-defined values.  A boundary (NEE) cell also holds, in each slot q its
+ * fluid neighbour B + e_q pulls, that neighbour's NEE value; its other slots, and wall cells'
+ * slots where bounce-back is on the consumer side, are unspecified. */
 int lbm_get_f(lbm_ctx* ctx, float* f_soa);
 /* The reference mask codes this context runs on (geo_pre's output: 0 unused, -1 ghost, 1 wall,
  * 2 inlet, 3 outlet / lid, 4 or 3 fluid ...), raster nx*ny*nz over the local planes -- the

@@ -28,12 +28,28 @@ def vessel_mask(shape, seed, nballs=5):
     return m
 
 
-def stored_cells(geo):
-    """Cells whose populations agree in every storage mode: fluid and boundary (NEE) cells.
-    Compact rows (LBM_TUNE_COMPACT) keep no slots for the passive cells outside the row spans,
-    which lbm_get_f then reports as 0, and their one-cell path bounces back on the consumer side,
-    so it never writes wall slots; lbm.h defines only the fluid cells' values."""
-    return (geo != 0) & (geo != -1) & (geo != 1)
+# D3Q19 lattice vectors in the kernels' order (lbm_d3q19.hpp)
+E_Q = [(0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1), (1, 1, 0), (1, -1, 0),
+       (-1, 1, 0), (-1, -1, 0), (1, 0, 1), (1, 0, -1), (-1, 0, 1), (-1, 0, -1), (0, 1, 1), (0, -1, 1),
+       (0, 1, -1), (0, -1, -1)]
+
+
+def defined_slots(geo, f, fluid=4):
+    """The populations every storage mode and kernel path agrees on: all 19 of each fluid cell,
+    and of each boundary (NEE) cell B the slots q its fluid neighbour B + e_q pulls -- the NEE
+    values.  Compact rows (LBM_TUNE_COMPACT) keep no slots for the passive cells outside the row
+    spans (lbm_get_f reports 0), consumer-side bounce-back never writes wall slots, and the NEE
+    cells' other slots are unspecified (lanes holding an NEE cell store whole vectors for the
+    directions its face does not take); lbm.h defines only the fluid cells' values."""
+    fl = geo == fluid
+    nee = (geo != 0) & (geo != -1) & (geo != 1) & ~fl
+    out = [f[:, fl].ravel()]
+    for q, (ex, ey, ez) in enumerate(E_Q):
+        if q == 0:
+            continue
+        pulled = np.roll(fl, (-ez, -ey, -ex), axis=(0, 1, 2))  # B + e_q is fluid
+        out.append(f[q][nee & pulled])
+    return np.concatenate(out)
 
 
 def inlet_tables(shape, seed):
@@ -213,7 +229,7 @@ def test_groups_bitwise(gpu, knob, case):
             lat = build()
         shape = lat.launch_shape()
         hist = lat.step(12)
-        f = lat.f()[:, stored_cells(lat.geo())]
+        f = defined_slots(lat.geo(), lat.f())
         lat.close()
         return shape, f, hist
 
@@ -246,7 +262,7 @@ def test_one_cell_groups_default_bitwise(gpu, knob, case):
             lat = build()
         shape = lat.launch_shape()
         hist = lat.step(12)
-        f = lat.f()[:, stored_cells(lat.geo())]
+        f = defined_slots(lat.geo(), lat.f())
         lat.close()
         return shape, f, hist
 
