@@ -46,23 +46,45 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_CELL = 152    # 19 fp32 loads + 19 fp32 stores per fluid cell update
 
 
-def cpu_baseline(n: int = 512, steps: int = 1):
-    """Serial oracle (the reference algorithm restated in C, oracle/) pinned to ONE host core
-    (oracle/cpu_baseline.py: sched_setaffinity + OMP_NUM_THREADS=1), run as a child process:
-    `value` = LDC n^3, the bench workload itself, for `steps` steps (~12 s per 512^3 step);
-    `c1` = config C1, LDC 64^3, 200 fixed steps."""
-    import subprocess
+def start_cpu_baseline(n: int = 512, steps: int = 1, quick: bool = False):
+    """Start the serial CPU baseline (oracle/cpu_baseline.py) as a child process: the oracle (the
+    reference algorithm restated in C, oracle/) on bounded samples, each pinned to ONE host core
+    of its own (sched_setaffinity + OMP_NUM_THREADS=1), side by side with the GPU measurements
+    (the GPU process's host threads keep the other cores): LDC n^3, the bench workload itself,
+    for `steps` steps (~12 s per 512^3 step); C1 (LDC 64^3) 200 fixed steps and to convergence;
+    C2 (LDC 256^3) and C3 (Poiseuille 128 x 512 x 128) fixed-step samples."""
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    out = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), str(n), str(steps)],
-                         env=env, capture_output=True, text=True, timeout=900, check=True)
-    r = json.loads(out.stdout.strip().splitlines()[-1])
-    b, c1 = r["bench"], r["c1"]
-    return {"value": round(b["mlups"], 3), "unit": "MLUPS", "cores": 1, "kind": "port",
+    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), str(n), str(steps)]
+    return subprocess.Popen(cmd + (["--quick"] if quick else []), env=env, stdout=subprocess.PIPE, text=True)
+
+
+def finish_cpu_baseline(p, n: int = 512, timeout: float = 900.0):
+    """The `cpu_baseline` object from start_cpu_baseline's child: `value` = the bench workload's
+    sample (one core), the configs' samples beside it."""
+    out, _ = p.communicate(timeout=timeout)
+    if p.returncode != 0:
+        raise SystemExit(f"cpu baseline failed ({p.returncode})")
+    r = json.loads(out.strip().splitlines()[-1])
+    b = r["bench"]
+    line = {"value": round(b["mlups"], 3), "unit": "MLUPS", "cores": 1, "kind": "port",
             "sample": f"oracle/lbm_oracle.c (serial C port of the reference kernels, fp32, two-phase LDC) on LDC "
-                      f"{n}^3 (the bench workload), {steps} step(s) after set-up, {b['seconds']:.1f} s, pinned to "
-                      f"core {r['core']} (sched_setaffinity, OMP_NUM_THREADS=1), host CPU: {r['cpu']}",
-            "c1": {"mlups": round(c1["mlups"], 3), "workload": "config C1: LDC 64^3, 200 fixed steps",
-                   "seconds": c1["seconds"]}}
+                      f"{n}^3 (the bench workload), {b['steps']} step(s) after set-up, {b['seconds']:.1f} s, pinned to "
+                      f"core {r['core']} (sched_setaffinity, OMP_NUM_THREADS=1), host CPU: {r['cpu']}"}
+    names = {"c1": "config C1: LDC 64^3, 200 fixed steps",
+             "c1_converge": "config C1: LDC 64^3 to convergence (tol 1e-6, 50 hits; residual summed in fp64 as "
+                            "liblbm does, so the stop step is liblbm's)",
+             "c2": "config C2: LDC 256^3, 10 fixed steps (BASELINE.md 4: 1000 steps scaled down)",
+             "c3": "config C3: Poiseuille 128x512x128 (pipe along y), 20 fixed steps, MLUPS over box cells "
+                   "(mlups_nlattice: over the reference's stored cells)"}
+    for k, what in names.items():
+        if k in r:
+            e = {"mlups": round(r[k]["mlups"], 3), "workload": what, "seconds": r[k]["seconds"],
+                 "steps": r[k]["steps"], "core": r["cores"][k]}
+            if "mlups_nlattice" in r[k]:
+                e["mlups_nlattice"] = round(r[k]["mlups_nlattice"], 3)
+            line[k] = e
+    line["samples_run"] = "side by side, one core each"
+    return line
 
 
 def pmc_traffic(workload: str):
@@ -116,8 +138,10 @@ def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
     lat.profile(True)
     lat.step(min(steps, 200), history=False)
     st = lat.stats()
+    placement = lat.placement()
     lat.close()
     out = {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
+    out["ms_per_step"] = round(dt / steps * 1e3, 5)
     out["rows_along"] = "xy"[lay["row_axis"] - 1]
     out["active_chunks"] = lay["active_chunks"]
     out["cells_per_lane"] = shape["cells_per_lane"]
@@ -138,6 +162,11 @@ def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
             rl["traffic_over_algo"] = pmc.get("traffic_over_algo")
             rl["traffic_source"] = f"profiles/pmc_traffic.json ({pmc.get('tag')}, tools/pmc_lattices.sh)"
         out["roofline"] = rl
+    # where the time of a two-buffer lattice goes: k_step by the buffer it reads (the other one
+    # is written), next to the write rates buffer_placement measured for its candidates
+    out["step_kernel_us_by_source_buffer"] = [
+        round(st[f"step_kernel_src{b}_ms"] / max(1, st[f"step_kernel_src{b}_launches"]) * 1e3, 2) for b in (0, 1)]
+    out["buffer_placement"] = placement
     return out
 
 
@@ -149,15 +178,15 @@ def config_lines(dev: int):
     lat, geo = cases.poiseuille(128, 512, 128, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
     k = "poiseuille_128x512x128 (C3)"
-    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200, name=k)
+    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 1000, name=k)
     # the same lattice on the x-row layout (lbm_desc.row_axis = 1), for comparison
     with lbm_amd.tuned(lbm_amd.TUNE_ROW_AXIS, 1):
         lat, geo = cases.poiseuille(128, 512, 128, device=dev)
-    out["poiseuille_128x512x128 (C3), x rows"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 200)
+    out["poiseuille_128x512x128 (C3), x rows"] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 1000)
     lat, geo, _, _ = cases.bifurcation(1, device=dev)
     nl, _ = lbm_amd.index_transform(geo)
     k = "bifurcation_64x83x32 (C4)"
-    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 2000, name=k)
+    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 4401, name=k)
     # SURVEY 8(d) C4's bandwidth-relevant sparse number: the shipped mask upsampled 4x per axis
     lat, raw = cases.bifurcation_upsampled(4, device=dev)
     nl, _ = lbm_amd.index_transform(lat.geo())
@@ -272,10 +301,22 @@ def check_rccl_ranks(rank: int, rccl_ranks: int, world: int):
         raise SystemExit(f"rank {rank}: RCCL communicator has {rccl_ranks} ranks, WORLD_SIZE {world}")
 
 
+def single_domain_ms(lat, steps: int, warm: int = 3) -> float:
+    """Wall ms per step of this rank's slab stepped as a single domain (no communicator yet: one
+    launch per step over all its planes, ghost planes left as initialised) -- the per-GPU work
+    of the slab without the halo exchange, the reference point of `weak_scaling_eff`."""
+    lat.step(warm, history=False)
+    lat.sync()
+    t = time.perf_counter()
+    lat.step(steps, history=False)
+    lat.sync()
+    return (time.perf_counter() - t) / steps * 1e3
+
+
 def gather_ranks(mine, elapsed: float, kern_ms: float, main_ms: float, n_fluid: int, world: int, group=None):
     """N > 1: the slowest rank's wall time and kernel times (max over ranks), the fluid cells of
     all slabs (sum) and every rank's row `mine` = [rank, rccl_ranks, edge, interior, halo,
-    halo_exposed, wall] (ms per step), gathered over torch.distributed (gloo)."""
+    halo_exposed, wall, single_domain] (ms per step), gathered over torch.distributed (gloo)."""
     elapsed, kern_ms, main_ms = ldist.max_over_ranks([elapsed, kern_ms, main_ms], group)
     n_fluid_total = int(ldist.sum_over_ranks([n_fluid], group)[0])
     every = [None] * world
@@ -283,20 +324,38 @@ def gather_ranks(mine, elapsed: float, kern_ms: float, main_ms: float, n_fluid: 
     return elapsed, kern_ms, main_ms, n_fluid_total, every
 
 
-def multi_gpu_block(every) -> dict:
+def multi_gpu_block(every, job_ms_per_step: float = None) -> dict:
     """The N > 1 bench line's `multi_gpu` object from the gathered per-rank rows: per-rank slab
     timings (HIP events, ms per step) -- edge-plane launch, interior launch, halo exchange on the
     communication stream, and the part of the halo that outlasted the interior launch (not
-    hidden) -- the smallest communicator any rank saw, and the hidden share of the halo."""
-    ranks = [{"rank": int(r[0]), "rccl_ranks": int(r[1]), "edge_ms": round(r[2], 4), "interior_ms": round(r[3], 4),
-              "halo_ms": round(r[4], 4), "halo_exposed_ms": round(r[5], 4), "wall_ms_per_step": round(r[6], 4)}
-             for r in sorted(every)]
+    hidden) -- the smallest communicator any rank saw, and the hidden share of the halo.
+    Weak scaling: each rank timed its own slab as a single domain before the communicator was
+    attached (single_domain_ms_per_step); weak_scaling_eff = that / the rank's slab wall time per
+    step, per rank and as the minimum, and for the job: the ranks' mean single-domain time / the
+    job's time per step (max over ranks, barrier-bracketed)."""
+    ranks = []
+    for r in sorted(every):
+        row = {"rank": int(r[0]), "rccl_ranks": int(r[1]), "edge_ms": round(r[2], 4), "interior_ms": round(r[3], 4),
+               "halo_ms": round(r[4], 4), "halo_exposed_ms": round(r[5], 4), "wall_ms_per_step": round(r[6], 4)}
+        if len(r) > 7 and r[7]:
+            row["single_domain_ms_per_step"] = round(r[7], 4)
+            row["weak_scaling_eff"] = round(r[7] / r[6], 4) if r[6] > 0 else None
+        ranks.append(row)
     halo = sum(r["halo_ms"] for r in ranks)
-    return {
+    out = {
         "rccl_ranks": min(r["rccl_ranks"] for r in ranks),
         "halo_hidden_frac": round(1.0 - sum(r["halo_exposed_ms"] for r in ranks) / halo, 4) if halo > 0 else None,
-        "per_rank": ranks,
     }
+    effs = [r["weak_scaling_eff"] for r in ranks if r.get("weak_scaling_eff") is not None]
+    if effs and len(effs) == len(ranks):
+        out["weak_scaling_eff_min"] = min(effs)
+        if job_ms_per_step:
+            single = sum(r["single_domain_ms_per_step"] for r in ranks) / len(ranks)
+            out["weak_scaling_eff_job"] = round(single / job_ms_per_step, 4)
+        out["weak_scaling_ref"] = ("each rank's own 512^3 slab stepped as one domain (no halo, no all-reduce) "
+                                   "on the same GPU in the same run, before lbm_attach_rccl")
+    out["per_rank"] = ranks
+    return out
 
 
 def main():
@@ -317,8 +376,15 @@ def main():
 
     n = args.n
     nzg = n * world
+    # the CPU baseline runs on its own host cores while the GPU is measured (N = 1 only)
+    cpu_proc = start_cpu_baseline() if world == 1 and not args.no_cpu_baseline else None
     lat = cases.ldc_device(n, n, n, z_offset=rank * n, nz_global=nzg, device=local)
+    single_ms = None
     if world > 1:
+        # the weak-scaling reference: this slab's step as a single domain on this GPU, then a
+        # fresh initial state for the slab run
+        single_ms = single_domain_ms(lat, max(5, min(args.steps, 20)))
+        lat.init_ldc()
         # a rank whose peer died fails its next wait with LBM_ERR_RCCL (async error poll, or
         # this limit) and exits non-zero, instead of hanging in a halo receive
         lbm_amd.tune(lbm_amd.TUNE_SYNC_TIMEOUT_S, 300)
@@ -349,7 +415,7 @@ def main():
     main_ms, main_n = st["step_kernel_ms"], max(1, st["step_kernel_launches"])
     per_step = lambda k: st[k + "_ms"] / args.steps  # noqa: E731
     mine = [rank, rccl_ranks, per_step("edge"), per_step("interior"), per_step("halo"), per_step("halo_exposed"),
-            elapsed / args.steps * 1e3]
+            elapsed / args.steps * 1e3, single_ms or 0.0]
     if world > 1:
         elapsed, kern_ms, main_ms, n_fluid_total, every = gather_ranks(mine, elapsed, kern_ms, main_ms,
                                                                       counts["n_fluid"], world)
@@ -443,15 +509,15 @@ def main():
         "kernel_src": lbm_amd.kernel_fingerprint(),
     }
     if world > 1:
-        line["multi_gpu"] = multi_gpu_block(every)
+        line["multi_gpu"] = multi_gpu_block(every, ms_step)
     if world == 1 and not args.no_secondary:
         line["secondary"] = {"ldc_64^3 (published config)": ldc_line(64, 2000, local, "ldc_64^3"),
-                             "ldc_256^3 (C2)": ldc_line(256, 200, local, "ldc_256^3 (C2)"),
+                             "ldc_256^3 (C2)": ldc_line(256, 1000, local, "ldc_256^3 (C2)"),
                              f"ldc{n}_random_velocity_start": perturbed_mlups(n, 50, local),
                              "ldc_512x512x4096 (C5 lattice, single domain)": c5_one_gpu(local),
                              **config_lines(local)}
-    if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline()
+    if cpu_proc is not None:
+        line["cpu_baseline"] = finish_cpu_baseline(cpu_proc)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -139,7 +139,10 @@ typedef struct {
  * (NEE values included), the step count and the convergence state -- to a file,
  * and back into a context created with the same descriptor (extent, slab, case, tau and
  * layout are checked; LBM_ERR_ARG otherwise).  A resumed run continues bit for bit.  Slab
- * contexts save and load one file per rank (ghost planes included).
+ * contexts save and load one file per rank (ghost planes included).  The file (format version 3)
+ * records whether the saving context bounced back on the consumer side (its wall slots were not
+ * written); a context that bounces back on the producer side restores them on load, so a file
+ * moves between the two modes (e.g. a one-cell device cavity and its LBM_TUNE_BOX = 1 twin).
  * A load that fails after the header checks (a truncated file) leaves the state unspecified. */
 int lbm_checkpoint_save(lbm_ctx* ctx, const char* path);
 int lbm_checkpoint_load(lbm_ctx* ctx, const char* path);
@@ -165,7 +168,7 @@ typedef enum {
   LBM_TUNE_EXACT_DIV = 2,       /* 1: the compiler's division by tau everywhere */
   LBM_TUNE_FUSED_RESIDUAL = 3,  /* 1 (default): the residual rides in the next step's launch */
   LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 (default) the two fastest-writing of up
-                                   to six allocations (lbm_buffer_placement), 1 the first two */
+                                   to sixteen allocations (lbm_buffer_placement), 1 the first two */
   LBM_TUNE_SYNC_TIMEOUT_S = 5,  /* RCCL contexts: a wait (lbm_sync, synchronising lbm_step, read-
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's
@@ -297,10 +300,11 @@ int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
 int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
 /* Placement of the two population buffers (not a reference interface).  HBM write bandwidth
  * differs between allocations (~5.5 vs ~6.4 TB/s for 10-GB buffers on MI355X, stable per
- * allocation); when a buffer is >= 1 GiB and the device has room, lbm_create allocates up to six
- * candidates, times one full-buffer write sweep of each and keeps the two fastest.  gbs[0..cap)
- * receives the candidates' rates (GB/s) in allocation order, *n their count (0: buffers under
- * 1 GiB, not probed), chosen[2] the indices kept.  Nullable outputs. */
+ * allocation); when a buffer is larger than 256 MB (the MALL) and the device has room,
+ * lbm_create allocates up to sixteen candidates (at most 64 GiB together: six at 512^3), times
+ * one full-buffer write sweep of each and keeps the two fastest.  gbs[0..cap) receives the
+ * candidates' rates (GB/s) in allocation order, *n their count (0: buffers of at most 256 MB,
+ * or compact rows, not probed), chosen[2] the indices kept.  Nullable outputs. */
 int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen);
 /* The device layout lbm_create chose (lbm_desc.row_axis / x_align resolved): row_axis 1 = x,
  * 2 = y; pitch = row slots; x_align 1..4; active_chunks = 256-cell chunks k_step launches a
@@ -344,6 +348,10 @@ int lbm_probe_stream_shapes(int device, int64_t bytes, int reps, double* gbs_sha
  * RCCL on a communication stream, overlapped with the interior update, and all-reduces the
  * residual sum. */
 int lbm_rccl_unique_id(uint8_t out_id[128]);
+/* A context in compact rows (a sparse single-domain lattice, lbm_get_storage; LBM_TUNE_COMPACT)
+ * cannot attach: LBM_ERR_STATE (create it with LBM_TUNE_COMPACT = 1, or as slabs).  Steps taken
+ * before attaching may have bounced back on the consumer side; attaching first restores the wall
+ * slots of both population buffers, so read-outs and further steps continue bit for bit. */
 int lbm_attach_rccl(lbm_ctx* ctx, const uint8_t id[128], int rank, int nranks);
 /* rank and communicator size as RCCL reports them (ncclCommCount); 0 / 1 without RCCL.
  * A communicator aborted by a failed peer or a timed-out wait stays failed: from then on

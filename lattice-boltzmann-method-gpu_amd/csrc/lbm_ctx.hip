@@ -185,6 +185,11 @@ struct lbm_ctx {
   // step k's source buffer holds wall slots that must be pulled raw (MainArgs::bb_raw): the
   // first step of a case whose walls do not bounce back at step 0
   bool bb_raw(int k) const { return k == 0 && !bb_immediate; }
+  // The wall slots of both buffers were not written by the steps that produced them: a step ran
+  // with bounce-back on the consumer side (or a checkpoint saved by such a context was loaded).
+  // Every producer-side reader -- the RCCL slab step, lbm_group_step, the lazy macros of a
+  // producer-side context -- first restores them (prime_walls).
+  bool walls_stale = false;
   std::string err;
 };
 
@@ -839,6 +844,25 @@ int reset_state(lbm_ctx* c) {
   c->cur = 0;
   c->halo_primed = false;
   c->macros_stale = false;
+  c->walls_stale = false;
+  return LBM_OK;
+}
+
+// Restore the wall slots a consumer-side step left unwritten (lbm_ctx::walls_stale) before a
+// producer-side reader pulls them: in both buffers, slot q of wall W = c - e_q gets cell c's own
+// slot opp(q) of the same buffer -- the value the producer side stores there (its post-collision
+// f_opp(q), Poiseulle.cu:601-746).  buf[cur] feeds the next step; buf[cur ^ 1], the last step's
+// source, feeds the lazy macros -- except after a single raw first step (no bounce-back at step
+// 0, MainArgs::bb_raw), whose source keeps its initial wall slots.  Compact rows always bounce
+// back on the consumer side and never get here.
+int prime_walls(lbm_ctx* c) {
+  if (!c->walls_stale || c->compact) return LBM_OK;
+  const Layout& L = c->L;
+  HIPCK(c, launch_bb_prime(c->buf[c->cur], c->type, c->links, L.ncell, L.pitch, L.plane, L.swap, c->s_comp));
+  if (c->steps_done >= 2 || c->bb_immediate)
+    HIPCK(c, launch_bb_prime(c->buf[c->cur ^ 1], c->type, c->links, L.ncell, L.pitch, L.plane, L.swap, c->s_comp));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  c->walls_stale = false;
   return LBM_OK;
 }
 
@@ -853,18 +877,28 @@ int reset_state(lbm_ctx* c) {
 // When the device has room (hipMemGetInfo, after `others` bytes for the remaining arrays), up to
 // four extra candidates are allocated, each zeroed and timed over one full-buffer sweep of
 // non-temporal 16-B stores, and the two fastest kept; the rest are freed before any other array
-// is allocated.  Lattices under 1 GiB per buffer (L2 / MALL resident, latency-bound) and
-// LBM_TUNE_BUFFER_ALLOC = 1 take the first two allocations (the latter still timed, for A/B).
+// is allocated.  Every buffer larger than the 256-MB MALL is probed (round 4 probed only
+// buffers >= 1 GiB, so the 647-MB buffers of the C3 pipe took whatever came first); smaller
+// ones (MALL resident, latency-bound) and LBM_TUNE_BUFFER_ALLOC = 1 take the first two
+// allocations (the latter still timed, for A/B).
+// The candidates take at most kPlacementBudget bytes together (six at 512^3) and number at most
+// kMaxCand: at LDC 256^3 (1.28-GB buffers) one or two of six candidates wrote at ~6.1 TB/s and
+// the rest at 4.9-5.6, so the step that writes the slower kept buffer ran 433 instead of 422 us,
+// and the first two allocations (no probe) 457 us (gpurun_out/r05a, tools/ab_alloc.py); more
+// candidates make a pair of fast ones likelier.
+constexpr size_t kPlacementMinBytes = (size_t)256 << 20;
+constexpr size_t kPlacementBudget = (size_t)64 << 30;
 hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
-  constexpr int kMaxCand = 6;
+  constexpr int kMaxCand = 16;
   int ncand = 2;
-  const bool probe = bytes >= ((size_t)1 << 30);
+  const bool probe = bytes > kPlacementMinBytes;
   if (!g_tune[LBM_TUNE_BUFFER_ALLOC] && probe) {
     size_t fr = 0, tot = 0;
     hipError_t e = hipMemGetInfo(&fr, &tot);
     if (e != hipSuccess) return e;
     const size_t need = 2 * bytes + others;
-    if (fr > need) ncand = (int)std::min<size_t>(kMaxCand, 2 + (fr - need) / bytes);
+    const int cap = (int)std::max<size_t>(2, std::min<size_t>(kMaxCand, kPlacementBudget / bytes));
+    if (fr > need) ncand = (int)std::min<size_t>(cap, 2 + (fr - need) / bytes);
   }
   std::vector<float*> p;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -965,7 +999,7 @@ int build_compact(lbm_ctx* c, const std::vector<uint8_t>& t, const std::vector<u
   gstart[R] = cum;
   const int64_t ncell = (4 * cum + kChunk - 1) / kChunk * kChunk, nchunk = ncell / kChunk;
   const int64_t guard = (n0 + 16 + kChunk - 1) / kChunk + 1;  // |offsets| of any lane's address
-  if (cum == 0 || (nchunk + 2 * guard) * kQ * kChunk >= (int64_t(1) << 31)) return LBM_OK;
+  if (cum == 0 || (nchunk + 2 * guard) * kQ * kChunk >= kCompactMaxFloats) return LBM_OK;
   if (g_tune[LBM_TUNE_COMPACT] == 0 && (double)ncell > 0.6 * (double)L.ncell) return LBM_OK;
   row_of.resize(ncell / 4, row_of.back());  // the padding groups of the last chunk: the last row
   std::vector<int> cmap(ncell, -1);
@@ -1661,6 +1695,8 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr, b
 }
 
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
+  if (c->bb_pull()) c->walls_stale = true;  // the whole-domain steps below store no wall slots
+  else RCK(prime_walls(c));
   if (c->sum_mode == LBM_SUM_CUB_TREE) {
     // the reference's order: per step calc_vel_square's terms into reference storage order, then
     // thrust::reduce's CUB tree in fp32 (ldc.cu:660-668)
@@ -1724,6 +1760,7 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
 // launch instead of preceding it (round 2: edge launch, interior launch and the two reduction
 // launches in series on s_comp).
 int step_rccl(lbm_ctx* c, int nsteps, bool want_hist) {
+  RCK(prime_walls(c));  // producer-side bounce-back from here on
   RCK(ensure_halo_buffers(c));
   if (!c->slab_part) HIPCK(c, hipMalloc(&c->slab_part, sizeof(double) * 2 * std::max(1, c->npart_slab)));
   // s_comm starts after whatever s_comp holds (set-up, a checkpoint load, read-outs)
@@ -1826,6 +1863,7 @@ int refresh_macros(lbm_ctx* c) {
     RCK(stage_dense(c, st, &src));
     RCK(to_dense(c, c->cur ^ 1, src));
   }
+  if (!c->bb_pull()) RCK(prime_walls(c));  // a producer-side read-out pulls the wall slots
   // the last step ran from this buffer: step h.k - 1
   const uint32_t* bbl = (c->bb_pull() && !c->bb_raw(h.k - 1)) ? c->links : nullptr;
   HIPCK(c, launch_moments(src, c->type, bbl, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch,
@@ -1988,11 +2026,13 @@ struct CkptHeader {
   char magic[8];  // "LBMCKPT1"
   int32_t version, nx, ny, nz, z_offset, nz_global, case_kind, swap, pitch, xshift, steps_done, cur;
   int32_t halo_primed;  // the ghost planes hold the exchange state (all 19 populations only at step 0)
+  int32_t walls_stale;  // saved by a context bouncing back on the consumer side: the wall slots of both
+                        // buffers were not written (lbm_ctx::walls_stale; version 3)
   uint32_t tau_bits;
   int64_t ncell, buf_floats;
   ConvState conv;
 };
-constexpr int32_t kCkptVersion = 2;
+constexpr int32_t kCkptVersion = 3;
 
 constexpr size_t kCkptSlice = (size_t)64 << 20;  // bytes staged through the host per copy
 
@@ -2009,6 +2049,7 @@ int lbm_checkpoint_save(lbm_ctx* c, const char* path) {
   h.swap = c->L.swap; h.pitch = c->L.pitch; h.xshift = c->L.xshift;
   h.steps_done = c->steps_done; h.cur = c->cur;
   h.halo_primed = c->halo_primed ? 1 : 0;
+  h.walls_stale = c->walls_stale ? 1 : 0;
   std::memcpy(&h.tau_bits, &c->tau, 4);
   h.ncell = c->compact ? c->ncell_c : c->L.ncell;
   h.buf_floats = c->pop_floats();
@@ -2059,7 +2100,8 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
                h.ncell == (c->compact ? c->ncell_c : c->L.ncell) && h.buf_floats == c->pop_floats();
   // run state of a well-formed file: one of the two buffers current, flags 0/1, the device
   // step counter equal to the host's
-  const bool sane = (h.cur == 0 || h.cur == 1) && h.steps_done >= 0 && (h.halo_primed == 0 || h.halo_primed == 1) && h.conv.k == h.steps_done &&
+  const bool sane = (h.cur == 0 || h.cur == 1) && h.steps_done >= 0 && (h.halo_primed == 0 || h.halo_primed == 1) &&
+                    (h.walls_stale == 0 || h.walls_stale == 1) && h.conv.k == h.steps_done &&
                     h.conv.tol_count >= 0 && h.conv.stopped >= 0 && h.conv.stopped <= 2;
   if (match && !sane) {
     std::fclose(f);
@@ -2111,6 +2153,10 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
   // crossing populations are exchanged, and a ghost wall's other slots hold this slab's
   // bounce-back values, which a fresh 19-population exchange would overwrite
   c->halo_primed = h.halo_primed != 0;
+  // a file from a consumer-side context has stale wall slots; a producer-side context restores
+  // them now (its next step pulls them), a consumer-side one never reads them
+  c->walls_stale = h.walls_stale != 0;
+  if (!c->bb_pull()) RCK(prime_walls(c));
   return LBM_OK;
 }
 
@@ -2326,14 +2372,11 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
              "lbm_tune(LBM_TUNE_COMPACT, 1))";
     return LBM_ERR_STATE;
   }
-  if (c->bb_pull() && c->steps_done > 0) {
-    // the steps so far bounced back on the consumer side and wrote no wall slots; the slab
-    // sequence's producer side reads them from the next step on: store them once from the
-    // current state, as its last step's producers would have
-    HIPCK(c, launch_bb_prime(c->buf[c->cur], c->type, c->links, c->L.ncell, c->L.pitch, c->L.plane, c->L.swap,
-                             c->s_comp));
-    HIPCK(c, hipStreamSynchronize(c->s_comp));
-  }
+  // the steps so far may have bounced back on the consumer side and written no wall slots; the
+  // slab sequence's producer side pulls them from the next step on, and a read-out before that
+  // step computes the macros producer-side from the last step's source: both buffers get them
+  // once from the current state, as the producers would have stored them (prime_walls)
+  RCK(prime_walls(c));
   NCCK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
   c->nranks = nranks;
@@ -2400,6 +2443,12 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
   for (int i = 0; i < n; ++i) {
     HIPCK(c0, hipStreamSynchronize(cs[i]->s_comp));
     RCK(ensure_halo_buffers(cs[i]));
+    // the slab ranges bounce back on the producer side: a context that stepped its whole domain
+    // consumer-side first gets its wall slots back
+    if (prime_walls(cs[i]) != LBM_OK) {
+      c0->err = cs[i]->err;
+      return LBM_ERR_HIP;
+    }
   }
   ConvState** dconvs = nullptr;
   HIPCK(c0, hipMalloc(&dconvs, sizeof(ConvState*) * n));

@@ -103,6 +103,15 @@ constexpr int64_t cell_off(int pitch, int64_t plane) {
 // (lbm_create keeps their buffers, guards included, under 2^31 floats)
 __device__ __forceinline__ int64_t fidx(int64_t c, int q) { return aidx(c, q); }
 __device__ __forceinline__ int fidx(int c, int q) { return ((c >> 8) * kQ + q) * kChunk + (c & (kChunk - 1)); }
+// a compact cell id as the 32-bit index of the compact paths (kCompactMaxFloats bounds every id
+// of a compact buffer); -DLBM_DEBUG_INDEX traps on an id outside that bound instead of letting
+// a 32-bit offset wrap
+__device__ __forceinline__ int compact_id(int64_t c) {
+#ifdef LBM_DEBUG_INDEX
+  if (c < -int64_t(kChunk) * 64 || ((c >> 8) * kQ + kQ) * kChunk > kCompactMaxFloats) __builtin_trap();
+#endif
+  return (int)c;
+}
 
 struct AddrD {
   int64_t c;
@@ -139,7 +148,7 @@ struct Rows {
     R.rb[0] = x.x; R.rb[1] = x.y; R.rb[2] = x.z; R.rb[3] = x.w;
     R.rb[4] = y.x; R.rb[5] = y.y; R.rb[6] = y.z; R.rb[7] = y.w;
     R.rb[8] = z.x;
-    R.s0 = (int)c - R.rb[4];
+    R.s0 = compact_id(c) - R.rb[4];
     return R;
   }
 };
@@ -662,7 +671,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
         OwnLds& L = own_lds[threadIdx.x >> 6];
         const uint32_t lm = m0 | m1 | m2 | m3;
         const bool walls = __any(lm != 0u);  // wave-uniform
-        if (walls) bb_own_issue_all(a.src, (int)c, lm, L, AllQ{});
+        if (walls) bb_own_issue_all(a.src, compact_id(c), lm, L, AllQ{});
         pull4_compose<SW>(v, e, take_lo, take_hi, AllQ{});
         if (walls) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes are in
@@ -1066,7 +1075,7 @@ __device__ __forceinline__ double process_compact_cell1(const MainArgs& a, int64
   float f[kQ];
   // consumer-side bounce-back: the wall links select the cell's own slots (no wall stores below)
   const uint32_t wl = (a.bb_pull && !a.bb_raw && fluid && (t & kWallAdj)) ? links : 0u;
-  pull1_bb<SW>(f, a.src, R, (int)c, wl, AllQ{});
+  pull1_bb<SW>(f, a.src, R, compact_id(c), wl, AllQ{});
   BcSlots bc{};
   if (a.bc_uniform) {
     bc = BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const};
@@ -1101,7 +1110,7 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   A ad;
   if constexpr (COMPACT) {
     const int row = a.cell_row[i];
-    pull1_bb<SW>(f, a.src, Rows::load(a.rowrec, c, row), (int)c, consumer ? links : 0u, AllQ{});
+    pull1_bb<SW>(f, a.src, Rows::load(a.rowrec, c, row), compact_id(c), consumer ? links : 0u, AllQ{});
     ad = RowsRef{a.rowrec, c, row};
   } else {
     ad = AddrD{c, a.pitch, a.plane};

@@ -25,6 +25,14 @@ __host__ __device__ __forceinline__ int64_t aidx(int64_t c, int q) {
   return ((c >> 8) * kQ + q) * kChunk + (c & (kChunk - 1));
 }
 
+// Compact rows (sparse single-domain lattices) index their population buffers with 32-bit float
+// offsets: lbm_create builds them only while a buffer, guard chunks included, holds fewer than
+// kCompactMaxFloats floats (build_compact), so every compact cell id c satisfies
+// (c / 256 * 19 + 18) * 256 + 255 < 2^31.  The dense box uses 64-bit offsets: a 32-bit one
+// overflows past ~113 M cells (2^31 floats / 19) -- the C5 lattice as one domain has 1.07 G; a
+// lab kernel that passed a dense cell as int faulted there in round 4.
+constexpr int64_t kCompactMaxFloats = int64_t(1) << 31;
+
 struct Layout {
   int nx, ny, nz;
   int xshift;         // cell (x, y, zs) lives at x - xshift + y*pitch + zs*plane: puts the

@@ -592,9 +592,9 @@ class Lattice:
     def placement(self):
         """Population-buffer placement (lbm_buffer_placement): candidates' write rates (GB/s) and
         the two kept; an empty list when the first two allocations were taken unprobed."""
-        gbs, n, ch = (C.c_double * 8)(), C.c_int(), (C.c_int * 2)()
-        self._ck(lbm_lib().lbm_buffer_placement(self.h, gbs, 8, C.byref(n), ch), "lbm_buffer_placement")
-        return {"candidate_write_gbs": [round(gbs[i], 1) for i in range(min(n.value, 8))], "chosen": [ch[0], ch[1]]}
+        gbs, n, ch = (C.c_double * 16)(), C.c_int(), (C.c_int * 2)()
+        self._ck(lbm_lib().lbm_buffer_placement(self.h, gbs, 16, C.byref(n), ch), "lbm_buffer_placement")
+        return {"candidate_write_gbs": [round(gbs[i], 1) for i in range(min(n.value, 16))], "chosen": [ch[0], ch[1]]}
 
     def profile(self, enabled: bool = True):
         self._ck(lbm_lib().lbm_profile(self.h, 1 if enabled else 0), "lbm_profile")

@@ -86,8 +86,9 @@ def _worker(rank, world, port, out_dir, rccl):
     b = _bench()
     b._imports()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    # fake per-rank slab statistics: [rank, rccl_ranks, edge, interior, halo, halo_exposed, wall] ms/step
-    mine = [rank, rccl[rank], 0.03 + rank, 3.4, 0.05 * (rank + 1), 0.01 * rank, 3.5 + rank]
+    # fake per-rank slab statistics: [rank, rccl_ranks, edge, interior, halo, halo_exposed, wall,
+    # single-domain] ms/step
+    mine = [rank, rccl[rank], 0.03 + rank, 3.4, 0.05 * (rank + 1), 0.01 * rank, 3.5 + rank, 3.3 + 0.1 * rank]
     res = {}
     try:
         b.check_rccl_ranks(rank, rccl[rank], world)
@@ -97,7 +98,7 @@ def _worker(rank, world, port, out_dir, rccl):
     el, km, mm, nf, every = b.gather_ranks(mine, 1.0 + rank, 10.0 * (rank + 1), 5.0 + rank, 1000 + rank, world)
     res.update(elapsed=el, kern_ms=km, main_ms=mm, n_fluid=nf)
     if rank == 0:
-        res["multi_gpu"] = b.multi_gpu_block(every)
+        res["multi_gpu"] = b.multi_gpu_block(every, 4.5)
     json.dump(res, open(os.path.join(out_dir, f"w{rank}.json"), "w"))
     dist.barrier()
     dist.destroy_process_group()
@@ -122,3 +123,18 @@ def test_multi_gpu_report_gloo(tmp_path, rccl):
     assert mg["per_rank"][1]["edge_ms"] == 1.03 and mg["per_rank"][1]["wall_ms_per_step"] == 4.5
     # exposed 0.00 + 0.01 ms of a 0.05 + 0.10 ms halo: hidden share 1 - 0.01 / 0.15
     assert mg["halo_hidden_frac"] == round(1 - 0.01 / 0.15, 4)
+    # weak scaling against each rank's own slab stepped as one domain: 3.3 / 3.5 and 3.4 / 4.5
+    assert [p["weak_scaling_eff"] for p in mg["per_rank"]] == [round(3.3 / 3.5, 4), round(3.4 / 4.5, 4)]
+    assert mg["weak_scaling_eff_min"] == round(3.4 / 4.5, 4)
+    assert mg["weak_scaling_eff_job"] == round(3.35 / 4.5, 4)
+
+
+def test_cpu_baseline_assembly():
+    """The CPU baseline child (oracle/cpu_baseline.py) on a small sample: one pinned core per
+    sample, the bench workload's sample as `value`, C1 beside it."""
+    b = _bench()
+    line = b.finish_cpu_baseline(b.start_cpu_baseline(24, 3, quick=True), n=24)
+    assert line["value"] > 0 and line["cores"] == 1 and line["kind"] == "port"
+    assert "LDC 24^3" in line["sample"] and "3 step(s)" in line["sample"]
+    assert line["c1"]["steps"] == 200 and line["c1"]["mlups"] > 0
+    assert "c2" not in line and "c1_converge" not in line  # --quick

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Build liblbm.so lab variants for interleaved A/B (tools/ab_lattices.py) into tools/ab/<name>/.
+
+    python3 tools/lab_build.py <name> <patch>[,<patch>...]
+
+A patch is a named list of literal (file, old, new) edits applied to a copy of csrc/ (the
+product sources stay untouched); the copy is built with the product's flags.  Lab variants
+are measurement tools: several compute wrong values on purpose (they remove work to price it).
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "lattice-boltzmann-method-gpu_amd")
+
+PATCHES = {
+    # WRONG VALUES: 4-cell ranges launch no NEE blocks (the NEE neighbours' slots go unwritten)
+    "no_nee_blocks": [("lbm_ctx.hip", "  r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);",
+                       "  r.nee_blocks = 0;\n  r.n_nee = 0;")],
+    # WRONG VALUES: chunk waves store no bounce-back slots
+    "no_bb": [("lbm_kernels.hip", "  if (!consumer && __any(t4 & kWall4)) {  // wave-uniform",
+               "  if (false) {  // lab: no bounce-back stores"),
+              ("lbm_kernels.hip", "  if (!consumer && (t4 & kWall4)) {  // rare, divergent",
+               "  if (false) {  // lab")],
+}
+
+
+def main():
+    name, specs = sys.argv[1], sys.argv[2].split(",")
+    tmp = tempfile.mkdtemp(prefix="lab_")
+    try:
+        src = os.path.join(tmp, "pkg", "csrc")  # csrc/../../include/lbm.h as in the tree
+        shutil.copytree(os.path.join(PKG, "csrc"), src)
+        os.symlink(os.path.join(REPO, "include"), os.path.join(tmp, "include"))
+        for spec in specs:
+            for fname, old, new in PATCHES[spec]:
+                p = os.path.join(src, fname)
+                text = open(p).read()
+                if text.count(old) != 1:
+                    raise SystemExit(f"patch {spec}: {fname}: pattern found {text.count(old)} times")
+                open(p, "w").write(text.replace(old, new))
+        out = os.path.join(REPO, "tools", "ab", name)
+        os.makedirs(out, exist_ok=True)
+        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
+               "-fhip-fp32-correctly-rounded-divide-sqrt", "-I", os.path.join(REPO, "include"), "-shared", "-o",
+               os.path.join(out, "liblbm.so"), os.path.join(src, "lbm_kernels.hip"), os.path.join(src, "lbm_ctx.hip"),
+               "-L/opt/rocm/lib", "-lrccl", "-lrocprofiler-sdk-roctx"]
+        subprocess.check_call(cmd)
+        print(f"built tools/ab/{name}/liblbm.so ({','.join(specs)})")
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
