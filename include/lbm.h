@@ -199,7 +199,13 @@ typedef enum {
                                    compute cell types and wall links from coordinates, and its
                                    one-cell single-domain range bounces back on the consumer side;
                                    1 they load them like any lattice's */
-  LBM_TUNE_COUNT = 12
+  LBM_TUNE_NEE_FIX = 12,        /* NEE values of a single-domain 4-cell range whose chunk waves collide
+                                   its NEE-adjacent cells (the pipe's rows along y): 0 (default) one
+                                   small launch after the step kernel stores them from the cells'
+                                   (rho, u) the chunk waves recorded and their own post-collision
+                                   slots; 1 NEE blocks in the step launch re-pull and re-collide
+                                   every NEE-adjacent cell (round 4) */
+  LBM_TUNE_COUNT = 13
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

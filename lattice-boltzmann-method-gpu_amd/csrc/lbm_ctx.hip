@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -62,6 +62,11 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
   bool nee_chunks = false;  // 4-cell ranges: chunk waves also store the NEE-adjacent cells (MainArgs)
+  // single-domain nee_chunks ranges (LBM_TUNE_NEE_FIX): no NEE blocks; the chunk waves record the
+  // NEE-adjacent cells' (rho, u) in lbm_ctx::nee_mac and k_nee_fix stores the NEE values after the
+  // step launch, from those records and the cells' own post-collision slots (cells, cell_nl and
+  // nee_bc are its list)
+  bool nee_fix = false;
   // one-cell ranges whose waves all fit on the device at once: the fused residual's blocks go
   // last (MainArgs::red_last), so that no chunk wave waits for a slot behind them (LDC 64^3
   // 11.30 -> 11.14 us, C4 8.48 -> 8.27 us; a grid of several rounds -- the coronary tree 36.0 ->
@@ -101,6 +106,7 @@ struct lbm_ctx {
   int8_t* codes = nullptr;               // reference codes per storage cell (lbm_get_geo)
   float *bc_in = nullptr, *bc_out = nullptr;  // inlet / outlet u_y tables (lbm_init_case)
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
+  float4* nee_mac = nullptr;  // whole.nee_fix: (rho, u) of the NEE-adjacent cells, per (compact) cell
   Range whole, edge, mid;  // single domain: whole; slabs: both edge planes (one launch), interior
   double* partial_all = nullptr;
   double* red_part = nullptr;  // fused residual (one-cell single domain): 2 x red_n partials by step parity
@@ -164,6 +170,8 @@ struct lbm_ctx {
   bool compact = false;
   int64_t ncell_c = 0, nchunk_c = 0, guard_c = 0;  // compact cell slots (whole chunks), guard chunks
   int* cmap = nullptr;     // device: the dense cell of every compact cell, -1 for none
+  std::vector<int> cmap_h; // its host copy (lbm_get_f places the compact slots on the host)
+  int* crow = nullptr;     // device: the storage row of every compact 4-cell group (k_moments_compact)
   int4* rowrec = nullptr;  // device: per storage row the nine neighbour-row offsets (MainArgs::rowrec)
   int4* grouprec = nullptr;  // device, one-cell compact ranges: rowrec of every compact group's row
   uint8_t* ctype = nullptr;
@@ -403,6 +411,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.cells = r.cells; a.cell_nl = r.cell_nl; a.nee_bc = r.nee_bc; a.n_nee = r.n_nee;
   a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
   a.nee_chunks = r.nee_chunks ? 1 : 0;
+  a.nee_mac = r.nee_fix ? c->nee_mac : nullptr;
   if (fr) {
     a.partial = fr->part;
     a.red_blocks = 8;
@@ -416,6 +425,9 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
     c->launches++;
     RCK(timed(c, st, kKindStep, kKindSrc0 + srcbuf, range_kind, [&] {
                 HIPCK(c, launch_step(a, st));
+                // the NEE values of this step, from what its chunk waves recorded (counted with the
+                // step kernel: one step's update is both launches)
+                if (r.nee_fix) HIPCK(c, launch_nee_fix(a, st));
                 return LBM_OK;
               },
               range_kind == kKindMid ? &c->last_mid_end : nullptr));
@@ -453,7 +465,8 @@ int upload(lbm_ctx* c, T** dev, const std::vector<T>& h) {
 // NEE-link masks k_flag_fluid wrote (the masks the kernels read, so the gathered boundary
 // records are indexed exactly as the kernels index them)
 int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<uint8_t>& t,
-                const std::vector<uint32_t>& nlk, int64_t lo2 = 0, int64_t hi2 = 0, const CompactView* cv = nullptr) {
+                const std::vector<uint32_t>& nlk, int64_t lo2 = 0, int64_t hi2 = 0, const CompactView* cv = nullptr,
+                bool single = false) {
   if (lo2 < hi) lo2 = hi2 = 0;  // overlapping second interval (single-plane slab): drop it
   r.c_lo = lo;
   r.c_hi = hi;
@@ -770,6 +783,13 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   }
   r.nee_waves = nee_waves_for(r.n_nee, contig);
   r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);
+  // the single-domain range of a lattice whose chunk waves collide the NEE-adjacent cells: their
+  // NEE values from k_nee_fix after the step launch instead of NEE blocks that pull and collide
+  // every such cell again (LBM_TUNE_NEE_FIX)
+  if (single && !r.quarter && r.nee_chunks && r.n_nee > 0 && g_tune[LBM_TUNE_NEE_FIX] != 1) {
+    r.nee_fix = true;
+    r.nee_blocks = 0;
+  }
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }
@@ -1050,6 +1070,8 @@ int build_compact(lbm_ctx* c, const std::vector<uint8_t>& t, const std::vector<u
       nlc[i] = nlk[cmap[i]];
     }
   RCK(upload(c, &c->cmap, cmap));
+  RCK(upload(c, &c->crow, row_of));
+  c->cmap_h = cmap;
   {
     int* p = nullptr;
     RCK(upload(c, &p, rec));
@@ -1088,7 +1110,7 @@ int build_compact(lbm_ctx* c, const std::vector<uint8_t>& t, const std::vector<u
   free_range(c->edge);
   free_range(c->mid);
   const CompactView cv{&cmap, &row_of, quarter};
-  return build_range(c, c->whole, 4 * gstart[n1], 4 * gstart[(int64_t)(L.nz + 1) * n1], tc, nlc, 0, 0, &cv);
+  return build_range(c, c->whole, 4 * gstart[n1], 4 * gstart[(int64_t)(L.nz + 1) * n1], tc, nlc, 0, 0, &cv, true);
 }
 
 }  // namespace
@@ -1100,7 +1122,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 1};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1351,7 +1373,8 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       }
     }
     const int64_t P = L.plane, nz = d.nz;
-    if (build_range(c, c->whole, P, (nz + 1) * P, t, nlk) != LBM_OK) return bail(LBM_ERR_HIP);
+    if (build_range(c, c->whole, P, (nz + 1) * P, t, nlk, 0, 0, nullptr, c->d.nz_global == d.nz) != LBM_OK)
+      return bail(LBM_ERR_HIP);
     if (build_range(c, c->edge, P, 2 * P, t, nlk, nz * P, (nz + 1) * P) != LBM_OK) return bail(LBM_ERR_HIP);
     if (build_range(c, c->mid, 2 * P, std::max(2 * P, nz * P), t, nlk) != LBM_OK) return bail(LBM_ERR_HIP);
     // compact rows for a single domain whose step takes group lists (vessel trees)
@@ -1367,6 +1390,10 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     if (c->fuse_red) {
       c->red_n = c->whole.npart + 8;
       CK(hipMalloc(&c->red_part, sizeof(double) * 2 * c->red_n));
+    }
+    if (c->whole.nee_fix) {  // per (compact) cell: only the NEE-adjacent cells' entries are used
+      const int64_t n = c->compact ? c->ncell_c : L.ncell;
+      CK(hipMalloc(&c->nee_mac, sizeof(float4) * n));
     }
     c->edge.part = c->whole.part + c->whole.npart;
     c->mid.part = c->edge.part + c->edge.npart;
@@ -1398,6 +1425,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->s_comp) (void)hipStreamSynchronize(c->s_comp);
   if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->nee_mac) (void)hipFree(c->nee_mac);
   for (float* p : {c->alloc[0], c->alloc[1], c->rho, c->ux, c->uy, c->uz, c->hist, c->send_up, c->send_dn,
                    c->recv_up, c->recv_dn})
     if (p) (void)hipFree(p);
@@ -1418,7 +1446,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->ref_idx) (void)hipFree(c->ref_idx);
   if (c->terms) (void)hipFree(c->terms);
   if (c->cub_part) (void)hipFree(c->cub_part);
-  for (void* p : {(void*)c->cmap, (void*)c->rowrec, (void*)c->grouprec, (void*)c->ctype, (void*)c->clinks, (void*)c->cnlinks,
+  for (void* p : {(void*)c->cmap, (void*)c->crow, (void*)c->rowrec, (void*)c->grouprec, (void*)c->ctype, (void*)c->clinks, (void*)c->cnlinks,
                   (void*)c->crho, (void*)c->cux, (void*)c->cuy, (void*)c->cuz})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1857,17 +1885,16 @@ int refresh_macros(lbm_ctx* c) {
   c->macros_stale = false;
   if (h.k == 0) return LBM_OK;  // no step ran: the initial arrays
   const Layout& L = c->L;
-  float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
-  Stage st;
-  if (c->compact) {  // its dense copy
-    RCK(stage_dense(c, st, &src));
-    RCK(to_dense(c, c->cur ^ 1, src));
-  }
+  const float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
   if (!c->bb_pull()) RCK(prime_walls(c));  // a producer-side read-out pulls the wall slots
   // the last step ran from this buffer: step h.k - 1
-  const uint32_t* bbl = (c->bb_pull() && !c->bb_raw(h.k - 1)) ? c->links : nullptr;
-  HIPCK(c, launch_moments(src, c->type, bbl, c->rho, c->ux, c->uy, c->uz, L.plane, (L.nz + 1) * L.plane, L.pitch,
-                          L.plane, L.swap, c->s_comp));
+  const bool consumer = c->bb_pull() && !c->bb_raw(h.k - 1);
+  if (c->compact)  // straight from the compact buffer, addressed as the step kernels address it
+    HIPCK(c, launch_moments_compact(src, c->ctype, consumer ? c->clinks : nullptr, c->cmap, c->crow, c->rowrec, c->rho,
+                                    c->ux, c->uy, c->uz, c->whole.c_lo, c->whole.c_hi, L.swap, c->s_comp));
+  else
+    HIPCK(c, launch_moments(src, c->type, consumer ? c->links : nullptr, c->rho, c->ux, c->uy, c->uz, L.plane,
+                            (L.nz + 1) * L.plane, L.pitch, L.plane, L.swap, c->s_comp));
   HIPCK(c, hipStreamSynchronize(c->s_comp));
   return LBM_OK;
 }
@@ -1996,17 +2023,27 @@ int lbm_get_f(lbm_ctx* c, float* f) {
   if (!c || !f) return LBM_ERR_ARG;
   RCK(lbm_sync(c));
   const Layout& L = c->L;
-  std::vector<float> h((size_t)L.nchunk * kQ * kChunk);
-  const float* cur = c->buf[c->cur];
-  Stage st;
-  if (c->compact) {  // the stored cells' populations into a dense copy
-    float* f = nullptr;
-    RCK(stage_dense(c, st, &f));
-    RCK(to_dense(c, c->cur, f));
-    HIPCK(c, hipStreamSynchronize(c->s_comp));
-    cur = f;
+  if (c->compact) {
+    // the compact buffer as it is, placed on the host through cmap (no dense device copy); cells
+    // outside the row spans hold no slots and read 0
+    std::vector<float> h((size_t)c->pop_floats());
+    HIPCK(c, hipMemcpy(h.data(), c->buf[c->cur], sizeof(float) * h.size(), hipMemcpyDeviceToHost));
+    std::vector<int> comp((size_t)L.ncell, -1);
+    for (size_t i = 0; i < c->cmap_h.size(); ++i)
+      if (c->cmap_h[i] >= 0) comp[c->cmap_h[i]] = (int)i;
+    for (int q = 0; q < kQ; ++q)
+      for (int z = 0; z < L.nz; ++z)
+        for (int y = 0; y < L.ny; ++y) {
+          float* row = f + (((int64_t)q * L.nz + z) * L.ny + y) * L.nx;
+          for (int x = 0; x < L.nx; ++x) {
+            const int i = comp[cell_of(L, x, y, z)];
+            row[x] = i >= 0 ? h[aidx(i, q)] : 0.0f;
+          }
+        }
+    return LBM_OK;
   }
-  HIPCK(c, hipMemcpy(h.data(), cur, sizeof(float) * h.size(), hipMemcpyDeviceToHost));
+  std::vector<float> h((size_t)L.nchunk * kQ * kChunk);
+  HIPCK(c, hipMemcpy(h.data(), c->buf[c->cur], sizeof(float) * h.size(), hipMemcpyDeviceToHost));
   for (int q = 0; q < kQ; ++q)
     for (int z = 0; z < L.nz; ++z)
       for (int y = 0; y < L.ny; ++y) {

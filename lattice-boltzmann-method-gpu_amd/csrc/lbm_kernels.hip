@@ -745,13 +745,21 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     const int64_t cj = c + j;
     // NEE-adjacent cells belong to the NEE blocks of the launch (nee_cell), unless the range
     // hands the chunk waves their own slots (nee_chunks: the NEE blocks then only add the NEE
-    // neighbours' slots)
+    // neighbours' slots, or, nee_mac, k_nee_fix does after the launch)
     const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
                     (a.nee_chunks || !(t & kNeeAdj));
     if (in) {
       store |= 1u << j;
       acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
     }
+  }
+  if (a.nee_mac != nullptr && __any(store != 0u && (t4 & kNee4) != 0u)) {  // wave-uniform
+    // the NEE-adjacent cells' (rho, u) of this step for k_nee_fix (one 16-B store per cell)
+    const f4 R{r0, r1, r2, r3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((store & (1u << j)) && ((t4 >> (8 * j)) & kNeeAdj))
+        a.nee_mac[c + j] = make_float4(R[j], UX[j], UY[j], UZ[j]);
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
   // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
@@ -1127,6 +1135,41 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   if (a.nee_chunks) return 0.0;  // the chunk wave stores the cell and sums its |u|
   fix_store_all<SW>(f, a.dst, c, ad, a.bb_pull ? 0u : links, AllQ{});
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
+}
+
+// NEE values after the step launch (MainArgs::nee_mac; single-domain 4-cell ranges whose chunk
+// waves collide the NEE-adjacent cells, nee_chunks): a chunk wave recorded each such cell's
+// (rho, u) of the step and stored its post-collision populations into its own slots of dst, so
+// one thread per NEE-adjacent cell stores the values boundary_stream writes into its NEE
+// neighbours (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021) -- the same values
+// nee_cell computes, without nee_cell's 19 scattered pulls and its second collision of the cell.
+// The prefactors RN(rho / d) by the exact division: the step's fast quotient is proven equal to
+// it wherever the step used it.
+template <int... Qs>
+__device__ __forceinline__ void own_slots(float* f, const float* __restrict__ dst, int64_t c, uint32_t nl,
+                                          std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = ((nl >> Qs) & 1u) ? dst[fidx(c, Qs)] : 0.0f), ...);
+}
+template <bool SW, bool COMPACT>
+__global__ __launch_bounds__(kBlock) void k_nee_fix(const MainArgs a) {
+  if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step was a no-op
+  const int i = blockIdx.x * kBlock + (int)threadIdx.x;
+  if (i >= a.n_nee) return;
+  const int64_t c = a.cells[i];
+  const uint32_t nl = a.cell_nl[i];
+  const float4* rec = a.nee_bc + (int64_t)i * kNeeSlots;
+  const BcSlots bc = a.bc_uniform ? BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const}
+                                  : BcSlots{rec[0], rec[1], rec[2], rec[3], rec[4]};
+  const float4 m = a.nee_mac[c];
+  float f[kQ];
+  own_slots(f, a.dst, c, nl, AllQ{});
+  const Pref pre = Pref::exact(m.x);
+  if constexpr (COMPACT) {
+    const RowsRef ad{a.rowrec, c, a.cell_row[i]};
+    nee_store_all<SW>(a, ad.get(), nl, bc, Post1{f}, m.x, m.y, m.z, m.w, pre, AllQ{});
+  } else {
+    nee_store_all<SW>(a, AddrD{c, a.pitch, a.plane}, nl, bc, Post1{f}, m.x, m.y, m.z, m.w, pre, AllQ{});
+  }
 }
 
 // ---- the step kernel -------------------------------------------------------------------
@@ -1670,6 +1713,31 @@ __global__ void k_moments(const float* __restrict__ src, const uint8_t* __restri
   }
 }
 
+// the same read-out over compact rows (lbm_ctx::compact), without a dense staging copy: compact
+// cell i pulls through its row record (rowrec[row_of[i / 4]], as the step kernels address it)
+// and writes the dense cell cmap[i]'s macros
+template <bool SW>
+__global__ void k_moments_compact(const float* __restrict__ src, const uint8_t* __restrict__ type,
+                                  const uint32_t* bb_links, const int* __restrict__ cmap,
+                                  const int* __restrict__ row_of, const int4* __restrict__ rowrec, float* rho,
+                                  float* ux, float* uy, float* uz, int64_t lo, int64_t hi) {
+  for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t t = type[c];
+    const int d = cmap[c];
+    if ((t & kClassMask) != kFluid || d < 0) continue;
+    float f[kQ];
+    pull1_bb<SW>(f, src, Rows::load(rowrec, c, row_of[c >> 2]), compact_id(c),
+                 (bb_links && (t & kWallAdj)) ? bb_links[c] : 0u, AllQ{});
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) r = r + f[q];
+    rho[d] = r;
+    ux[d] = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / r;
+    uy[d] = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / r;
+    uz[d] = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / r;
+  }
+}
+
 // ---- reference-order fp32 residual (opt-in) -----------------------------------------------
 // calc_vel_square (ldc.cu:460-466): the step's |u| per fluid cell -- from the step's source
 // buffer, the same pulls and sums as the step (k_moments) -- into its reference storage slot
@@ -1933,6 +2001,17 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s) {
+  if (!a.nee_mac || a.n_nee <= 0) return hipSuccess;
+  const dim3 grid((a.n_nee + kBlock - 1) / kBlock);
+  typedef void (*Kern)(const MainArgs);
+  Kern k;
+  if (a.rowrec) k = a.swap ? k_nee_fix<true, true> : k_nee_fix<false, true>;
+  else k = a.swap ? k_nee_fix<true, false> : k_nee_fix<false, false>;
+  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_reduce(const double* partial, int n, double* scratch, ConvState* conv, float* hist_slot, int finish,
                          hipStream_t s, double* local_out) {
   if (!local_out) local_out = &conv->s_local;
@@ -2116,6 +2195,20 @@ hipError_t launch_moments(const float* src, const uint8_t* type, const uint32_t*
     hipLaunchKernelGGL(k_moments<true>, g, dim3(256), 0, s, src, type, bb_links, rho, ux, uy, uz, lo, hi, pitch, plane);
   else
     hipLaunchKernelGGL(k_moments<false>, g, dim3(256), 0, s, src, type, bb_links, rho, ux, uy, uz, lo, hi, pitch, plane);
+  return hipGetLastError();
+}
+
+hipError_t launch_moments_compact(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* cmap,
+                                  const int* row_of, const int4* rowrec, float* rho, float* ux, float* uy, float* uz,
+                                  int64_t lo, int64_t hi, int swap, hipStream_t s) {
+  if (hi <= lo) return hipSuccess;
+  const dim3 g(grid_for(hi - lo, 256));
+  if (swap)
+    hipLaunchKernelGGL(k_moments_compact<true>, g, dim3(256), 0, s, src, type, bb_links, cmap, row_of, rowrec, rho, ux,
+                       uy, uz, lo, hi);
+  else
+    hipLaunchKernelGGL(k_moments_compact<false>, g, dim3(256), 0, s, src, type, bb_links, cmap, row_of, rowrec, rho, ux,
+                       uy, uz, lo, hi);
   return hipGetLastError();
 }
 

@@ -120,6 +120,10 @@ struct MainArgs {
                             // own and bounce-back slots, |u|); the NEE blocks add only the NEE values
   int nee_blocks;           // multiple of 8 (keeps the chunk blocks' XCD order)
   int nee_waves;            // active waves per NEE block (1 for short, scattered lists)
+  float4* nee_mac;          // nullable (single-domain nee_chunks ranges, LBM_TUNE_NEE_FIX): the chunk
+                            // waves store each NEE-adjacent cell's (rho, ux, uy, uz) here, indexed by
+                            // cell; k_nee_fix (launch_nee_fix, after the step launch) reads them with
+                            // the cells' own post-collision slots and stores the NEE values
   int swap;             // 1: storage rows run along physical y (Layout::swap)
   // Compact rows (nullable; sparse single-domain lattices, group lists only): every per-cell
   // array above and the population buffers are indexed by compact cell ids -- storage row
@@ -180,6 +184,9 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
 };
 
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
+// after launch_step of a range with nee_mac: one thread per NEE-adjacent cell (cells, cell_nl,
+// nee_bc, n_nee) stores its NEE neighbours' slots of dst
+hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s);
 // NEE directions of a cell whose boundary data is loaded ahead (one flat face: 5); a cell
 // with more (edges and corners of several faces) loads the rest where they are used
 constexpr int kNeeSlots = 5;
@@ -220,6 +227,11 @@ hipError_t launch_cub_tree(const float* terms, int64_t n, int ipt, int vec, int 
 hipError_t launch_moments(const float* src, const uint8_t* type, const uint32_t* bb_links, float* rho, float* ux,
                           float* uy, float* uz, int64_t lo, int64_t hi, int pitch, int64_t plane, int swap,
                           hipStream_t s);
+// the same over compact rows: compact cells [lo, hi) pull through rowrec[row_of[c / 4]] and write
+// the macros of their dense cells cmap[c] (no dense staging copy of the population buffer)
+hipError_t launch_moments_compact(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* cmap,
+                                  const int* row_of, const int4* rowrec, float* rho, float* ux, float* uy, float* uz,
+                                  int64_t lo, int64_t hi, int swap, hipStream_t s);
 // per local plane digest of the fluid (rho, u) bits keyed by global coordinates (lbm_field_digest);
 // out[nz] must be zeroed
 hipError_t launch_digest(const uint8_t* type, const float* rho, const float* ux, const float* uy, const float* uz,

@@ -446,6 +446,33 @@ def test_poiseuille_c3_full_size_bitwise(gpu, oracle):
     assert o.bad_reads() == 0
 
 
+@pytest.mark.parametrize("nee_fix", [0, 1], ids=["nee_fix", "nee_blocks"])
+@pytest.mark.parametrize("shape", [(24, 40, 24), (33, 70, 29)])
+def test_poiseuille_nee_paths_bitwise(gpu, oracle, knob, nee_fix, shape):
+    """The pipe along y with four cells per lane: its chunk waves collide the NEE-adjacent cells
+    (nee_chunks), and the NEE values come either from k_nee_fix after the step launch (default)
+    or from NEE blocks that re-pull and re-collide those cells (LBM_TUNE_NEE_FIX 1).  Both bit for
+    bit against the oracle, populations included, through the convergence-free loop and a
+    convergence-controlled one (k_nee_fix skips converged no-op steps)."""
+    from lbm_amd import cases
+    import lbm_amd
+    knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)
+    knob(lbm_amd.TUNE_NEE_FIX, nee_fix)
+    nx, ny, nz = shape
+    lat, geo = cases.poiseuille(nx, ny, nz)
+    assert lat.layout()["row_axis"] == 2
+    o = fp64_sum(oracle.Oracle(oracle.POISEUILLE, geo, 0.58))
+    for s in (1, 2, 37):
+        hg, ho = lat.step(s), o.step(s)
+        assert_bitwise(lat, o, geo, 1, f"pipe {shape} +{s}")
+        assert_residuals(hg, ho)
+    lat.set_convergence(True, max_it=45, stag_max=50, tol=1e-6)
+    lat.step(20)
+    assert lat.state()["k"] == 46 and lat.state()["stopped"] == 1
+    o.step(6)
+    assert_bitwise(lat, o, geo, 1, f"pipe {shape} stopped at 46")
+
+
 def test_north_star_512_bitwise(gpu, oracle):
     """The north-star lattice itself (LDC 512^3, the bench's N = 1 workload, generated on the
     device as bench.py does) against the oracle on the host: (rho, u) bit for bit on all

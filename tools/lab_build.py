@@ -25,11 +25,14 @@ PATCHES = {
                "  if (false) {  // lab: no bounce-back stores"),
               ("lbm_kernels.hip", "  if (!consumer && (t4 & kWall4)) {  // rare, divergent",
                "  if (false) {  // lab")],
+    # a contiguous chunk list read from memory like a sparse one (prices the list load)
+    "force_list": [("lbm_ctx.hip", "    if (chunks[i] != chunks[0] + (int)i) r.chunk0 = -1;",
+                    "    if (chunks[i] != chunks[0] + (int)i) r.chunk0 = -1;\n  r.chunk0 = -1;")],
 }
 
 
 def main():
-    name, specs = sys.argv[1], sys.argv[2].split(",")
+    name, specs = sys.argv[1], [x for x in sys.argv[2].split(",") if x]
     tmp = tempfile.mkdtemp(prefix="lab_")
     try:
         src = os.path.join(tmp, "pkg", "csrc")  # csrc/../../include/lbm.h as in the tree
