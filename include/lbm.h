@@ -205,7 +205,10 @@ typedef enum {
                                    (rho, u) the chunk waves recorded and their own post-collision
                                    slots; 1 NEE blocks in the step launch re-pull and re-collide
                                    every NEE-adjacent cell (round 4) */
-  LBM_TUNE_COUNT = 13
+  LBM_TUNE_XCD_RUN = 13,        /* order of the step kernel's chunk workgroups over the 8 XCDs: 0 each
+                                   XCD takes one contiguous eighth of the chunks; L = 1..16 runs of
+                                   2^(L-1) workgroups, XCD x taking runs x, x + 8, x + 16, ... */
+  LBM_TUNE_COUNT = 14
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -182,6 +182,7 @@ struct lbm_ctx {
   // the device-generated cavity with power-of-two pitch and plane: the chunk kernels compute
   // types and links from coordinates (MainArgs::box)
   bool box = false;
+  int xcd_run = 0;  // MainArgs::xcd_run (LBM_TUNE_XCD_RUN at lbm_create)
   // bounce-back on the consumer side (MainArgs::bb_pull): compact ranges and the one-cell
   // whole-domain range of the cavity read a wall link's value from the cell's own opposite
   // slot, so no step writes wall slots.  Not the cavity's 4-cell range: its own-slice DMA made
@@ -398,6 +399,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
+  a.xcd_run = c->xcd_run;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
   a.groups = r.groups;
   a.ngroups = r.ngroups;
@@ -1122,7 +1124,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 1};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 1, 16};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1176,6 +1178,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   c->omc = 1.0f - 1.0f / d.tau;  // the reference's (1.0f - 1.0f / tau), evaluated in fp32
   c->fast_div = !g_tune[LBM_TUNE_EXACT_DIV] && verify_fast_div(d.tau);  // A/B: force the compiler's division
   c->bb_immediate = (d.case_kind == LBM_CASE_LDC);
+  c->xcd_run = g_tune[LBM_TUNE_XCD_RUN];
   Layout& L = c->L;
   L.nx = d.nx; L.ny = d.ny; L.nz = d.nz;
   L.swap = choose_swap(d);  // the caller's desc: c->d no longer holds geo / mask

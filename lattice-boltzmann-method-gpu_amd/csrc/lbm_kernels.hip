@@ -1228,7 +1228,17 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
     // L2), so logical block (b % 8) * (nb / 8) + b / 8 hands every XCD one contiguous run of
     // chunks and the lines two neighbouring chunks share stay in one L2 (-7% time at 512^3)
     const int b = bx - a.nee_blocks;  // red_blocks and nee_blocks are multiples of 8
-    slot = (b & 7) * (a.main_blocks >> 3) + (b >> 3);
+    const int per = a.main_blocks >> 3, k = b >> 3, x = b & 7;
+    if (a.xcd_run > 0) {
+      // runs of P = 2^(xcd_run - 1) blocks, the XCDs' runs interleaved (XCD x takes runs 8j + x):
+      // at any time the eight XCDs stream through neighbouring runs instead of eighths of the
+      // buffers far apart (LBM_TUNE_XCD_RUN); the tail of an XCD's share that does not fill a
+      // whole round of runs is split evenly as before
+      const int sh = a.xcd_run - 1, full = (per >> sh) << sh;
+      slot = k < full ? ((((k >> sh) << 3) + x) << sh) + (k & ((1 << sh) - 1)) : (full << 3) + x * (per - full) + (k - full);
+    } else {
+      slot = x * per + k;
+    }
     const int idx = slot * (WPB) + wave;
     if constexpr (QUARTER && COMPACT) {  // one cell per lane over compact rows, no list
       acc = process_compact_cell1<SW>(a, idx, lane);

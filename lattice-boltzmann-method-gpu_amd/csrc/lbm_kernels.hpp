@@ -93,6 +93,8 @@ struct MainArgs {
                               // records in group_rec, or -1
   const float4* group_rec;    // kNeeSlots records per cell of those groups (nee_prefetch's order)
   int main_blocks;      // multiple of 8 (XCD order), 0 without chunks
+  int xcd_run;          // 0: XCD x takes the x-th eighth of the chunk blocks; L > 0: runs of 2^(L-1)
+                        // blocks, XCD x taking runs 8j + x (LBM_TUNE_XCD_RUN)
   int chunk_stride;     // 1: each XCD's chunk waves loop over its eighth of the chunk list
                         // (lane-mask ranges only: k_step<..., MASK, STRIDE>)
   int quarter;          // 1: one cell per lane, a wave per 64-cell quarter chunk (small lattices)

@@ -11,7 +11,7 @@
 //          3: VMM -- the buffer assembled from 2-GiB handles, each mapped at its place.
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/alloc_lab.hip -o tools/alloc_lab
-//   tools/alloc_lab K GiB method
+//   tools/alloc_lab K GiB method [1: interleave periods of the XCD regions instead of windows]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -61,6 +61,39 @@ __global__ __launch_bounds__(256) void k_read(const f4* __restrict__ a, int64_t 
       if (i + k * 256 < hi) acc += __builtin_nontemporal_load(a + i + k * 256);
   }
   if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
+}
+
+// the same write sweep with the XCDs' regions interleaved at period S vectors: XCD x writes the
+// runs [(8j + x) S, (8j + x + 1) S), in order of j (S = n4 / 8: one contiguous region per XCD,
+// the sweep above and k_step's chunk order)
+__global__ __launch_bounds__(256) void k_write_s(f4* __restrict__ b, int64_t n4, int64_t S) {
+  const int xcd = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+  const int64_t per = n4 / 8;
+  const f4 v{0.f, 0.f, 0.f, 0.f};
+  for (int64_t t0 = (int64_t)lb * 1024 + threadIdx.x; t0 < per; t0 += (int64_t)nbx * 1024) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t t = t0 + k * 256;
+      if (t < per) __builtin_nontemporal_store(v, b + ((t / S) * 8 + xcd) * S + (t % S));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_copy_s(const f4* __restrict__ a, f4* __restrict__ b, int64_t n4, int64_t S) {
+  const int xcd = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+  const int64_t per = n4 / 8;
+  for (int64_t t0 = (int64_t)lb * 1024 + threadIdx.x; t0 < per; t0 += (int64_t)nbx * 1024) {
+    f4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t t = t0 + k * 256;
+      v[k] = t < per ? __builtin_nontemporal_load(a + ((t / S) * 8 + xcd) * S + (t % S)) : f4{};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t t = t0 + k * 256;
+      if (t < per) __builtin_nontemporal_store(v[k], b + ((t / S) * 8 + xcd) * S + (t % S));
+    }
+  }
 }
 
 int main(int argc, char** argv) {
@@ -114,6 +147,32 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     return ms / 3;
   };
+  if (argc > 4 && std::atoi(argv[4]) == 1) {  // interleave periods: write of each buffer, copy i -> i+1
+    const int64_t periods[] = {n4 / 8, (64 << 20) / 16, (16 << 20) / 16, (4 << 20) / 16, (2 << 20) / 16,
+                               (1 << 20) / 16, (256 << 10) / 16, (64 << 10) / 16, 81920, 5120};
+    for (int i = 0; i < K; ++i) {
+      const int j = (i + 1) % K;
+      std::printf("{\"buf\": %d, \"period_bytes\": [", i);
+      for (size_t p = 0; p < sizeof(periods) / sizeof(periods[0]); ++p)
+        std::printf("%s%lld", p ? ", " : "", (long long)periods[p] * 16);
+      std::printf("], \"write_tbs\": [");
+      for (size_t p = 0; p < sizeof(periods) / sizeof(periods[0]); ++p) {
+        const int64_t S = periods[p];
+        if ((n4 / 8) % S) { std::printf("%snull", p ? ", " : ""); continue; }  // S must divide an XCD's share
+        const float m = timeit([&] { hipLaunchKernelGGL(k_write_s, dim3(blocks), dim3(256), 0, 0, buf[i], n4, S); });
+        std::printf("%s%.3f", p ? ", " : "", bytes / m / 1e9);
+      }
+      std::printf("], \"copy_to_next_tbs\": [");
+      for (size_t p = 0; p < sizeof(periods) / sizeof(periods[0]); ++p) {
+        const int64_t S = periods[p];
+        if ((n4 / 8) % S) { std::printf("%snull", p ? ", " : ""); continue; }
+        const float m = timeit([&] { hipLaunchKernelGGL(k_copy_s, dim3(blocks), dim3(256), 0, 0, buf[i], buf[j], n4, S); });
+        std::printf("%s%.3f", p ? ", " : "", 2.0 * bytes / m / 1e9);
+      }
+      std::printf("]}\n");
+    }
+    return 0;
+  }
   const int64_t w4 = (int64_t)(piece / 16);
   for (int i = 0; i < K; ++i) {
     const float mw = timeit([&] { hipLaunchKernelGGL(k_write, dim3(blocks), dim3(256), 0, 0, buf[i], n4); });
