@@ -324,3 +324,37 @@ def test_compact_rows_vs_dense(gpu, knob, case, tmp_path):
         a.attach_rccl(lbm_amd.rccl_unique_id(), 0, 1)
     for lat in (a, b, c):
         lat.close()
+
+
+@pytest.mark.parametrize("path", ["bif_1cell_compact", "bif_4cell_compact", "ldc_1cell_box"])
+def test_consumer_side_steps_write_no_wall_slot(gpu, knob, path):
+    """With bounce-back on the consumer side no step writes a wall slot: every slot of every wall
+    cell keeps the sentinel it was set to, so no whole-vector or cell-by-cell store of a lane
+    holding a wall strays into it -- the check defined_slots cannot make, since it compares only
+    the slots the modes agree on."""
+    from lbm_amd import cases
+    import lbm_amd
+    if path == "bif_4cell_compact":
+        knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)
+        knob(lbm_amd.TUNE_GROUPS, 2)
+        knob(lbm_amd.TUNE_COMPACT, 2)
+    if path.startswith("bif"):
+        lat, geo, _, _ = cases.bifurcation(1)
+        assert lat.storage()["compact"]
+        wall, steps = geo == 1, 24
+    else:
+        lat = cases.ldc_device(32, 32, 32)
+        geo = lat.geo()
+        wall, steps = geo == 1, 23  # odd: buffer 1, which lbm_init's bounce-back priming of buffer 0 never touched
+    assert lat.launch_shape()["cells_per_lane"] == (4 if path == "bif_4cell_compact" else 1)
+    f = lat.f()
+    # distinct small values (the first step of the bifurcation pulls its walls raw)
+    sentinel = (0.01 + (np.arange(wall.sum() * 19).reshape(19, -1) % 1021) * 1e-5).astype(np.float32)
+    f[:, wall] = sentinel
+    lat.set_f(f)
+    lat.step(steps, history=False)
+    got = lat.f()[:, wall]
+    assert np.all(np.isfinite(lat.macros()[0][geo == (4 if path.startswith("bif") else 3)]))
+    bad = np.count_nonzero(got.view(np.uint32) != sentinel.view(np.uint32))
+    assert bad == 0, f"{path}: {bad} wall slots written"
+    lat.close()

@@ -28,6 +28,23 @@ PATCHES = {
     # a contiguous chunk list read from memory like a sparse one (prices the list load)
     "force_list": [("lbm_ctx.hip", "    if (chunks[i] != chunks[0] + (int)i) r.chunk0 = -1;",
                     "    if (chunks[i] != chunks[0] + (int)i) r.chunk0 = -1;\n  r.chunk0 = -1;")],
+    # WRONG VALUES: the NEE values are computed but not stored (prices the scattered 4-B stores)
+    "nee_nostore": [("lbm_kernels.hip", "      a.dst[fidx(nb, Q)] = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc, p.template of<Q>());",
+                     "      const float val = nee_value<Q>(fq, b, r, ux, uy, uz, a.omc, p.template of<Q>());\n"
+                     "      if (val == 1234.5678f) a.dst[fidx(nb, Q)] = val;")],
+    # ~140 extra VALU per chunk wave holding an NEE-adjacent cell, after its stores (prices an
+    # in-wave NEE tail; combine with no_nee_blocks + LBM_TUNE_NEE_FIX 1)
+    "valu_tail": [("lbm_kernels.hip", "  return acc;\n}\n\n// ---- one cell per lane",
+                   "  if (__any(t4 & kNee4)) {\n"
+                   "    float a2 = v[3][0] + v[7][1], u1 = UX[0], u2 = UY[0], u3 = UZ[0];\n"
+                   "#pragma unroll\n"
+                   "    for (int it = 0; it < 5; ++it) {\n"
+                   "      a2 = feq_pre<7>(a2, u1, u2, u3) + feq_pre<15>(a2 * 0.5f, u3, u1, u2) * a.omc;\n"
+                   "      u1 = u1 * 0.99f + a2 * 1e-9f;\n"
+                   "    }\n"
+                   "    if (a2 == 1234.5678f) a.dst[0] = a2;\n"
+                   "  }\n"
+                   "  return acc;\n}\n\n// ---- one cell per lane")],
 }
 
 

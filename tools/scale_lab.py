@@ -30,13 +30,17 @@ def kstep_us(lat, steps):
     return st["step_kernel_ms"] / st["step_kernel_launches"] * 1e3, nf, shape["main_blocks"]
 
 
+for kv in filter(None, os.environ.get("AB_TUNE", "").split(",")):  # "knob:value,...": lbm_tune
+    k, v = kv.split(":")
+    lbm_amd.tune(int(k), int(v))
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+only = os.environ.get("SCALE_ONLY", "")
 for r in range(rounds):
-    for L in (256, 512, 1024, 2048):
+    for L in (256, 512, 1024, 2048) if only != "ldc" else ():
         us, nf, mb = kstep_us(cases.poiseuille(128, L, 128)[0], 100)
         print(json.dumps({"round": r, "lattice": f"pipe 128x{L}x128", "k_step_us": round(us, 2), "n_fluid": nf,
                           "chunk_blocks": mb, "ns_per_kcell": round(us * 1e6 / nf, 3)}), flush=True)
-    for Z in (32, 64, 128, 256):
+    for Z in (32, 64, 128, 256) if only != "pipe" else ():
         us, nf, mb = kstep_us(cases.ldc_device(512, 512, Z), 50)
         print(json.dumps({"round": r, "lattice": f"ldc 512x512x{Z}", "k_step_us": round(us, 2), "n_fluid": nf,
                           "chunk_blocks": mb, "ns_per_kcell": round(us * 1e6 / nf, 3)}), flush=True)
