@@ -67,6 +67,14 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   // step launch, from those records and the cells' own post-collision slots (cells, cell_nl and
   // nee_bc are its list)
   bool nee_fix = false;
+  // single-domain chunk-list ranges with nee_chunks (LBM_TUNE_NEE_FIX 0): NEE records instead --
+  // the chunk waves compute the NEE values after their relaxation into lbm_ctx::nee_val and put
+  // them into the next step's pulls (MainArgs::nee_rec); per chunk-list entry the first record
+  // (nchunks + 1 prefix sums), n_rec records in chunk order
+  bool nee_records = false;
+  int* nee_rec_base = nullptr;
+  float4* nee_rec = nullptr;
+  int n_rec = 0;
   // one-cell ranges whose waves all fit on the device at once: the fused residual's blocks go
   // last (MainArgs::red_last), so that no chunk wave waits for a slot behind them (LDC 64^3
   // 11.30 -> 11.14 us, C4 8.48 -> 8.27 us; a grid of several rounds -- the coronary tree 36.0 ->
@@ -107,6 +115,10 @@ struct lbm_ctx {
   float *bc_in = nullptr, *bc_out = nullptr;  // inlet / outlet u_y tables (lbm_init_case)
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
   float4* nee_mac = nullptr;  // whole.nee_fix: (rho, u) of the NEE-adjacent cells, per (compact) cell
+  // whole.nee_records: the NEE values by step parity (2 x n_rec x 8 floats), and whether the NEE
+  // cells' slots of the two buffers miss them (steps since the last materialize_nee)
+  float* nee_val = nullptr;
+  bool nee_stale = false;
   Range whole, edge, mid;  // single domain: whole; slabs: both edge planes (one launch), interior
   double* partial_all = nullptr;
   double* red_part = nullptr;  // fused residual (one-cell single domain): 2 x red_n partials by step parity
@@ -414,6 +426,14 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
   a.nee_chunks = r.nee_chunks ? 1 : 0;
   a.nee_mac = r.nee_fix ? c->nee_mac : nullptr;
+  if (r.nee_records) {
+    const int64_t per = (int64_t)r.n_rec * 8;
+    a.nee_rec_base = r.nee_rec_base;
+    a.nee_rec = r.nee_rec;
+    a.nee_out = c->nee_val + (step & 1) * per;
+    // step 0 pulls the NEE cells' slots raw (boundary_stream runs after update)
+    a.nee_in = step > 0 ? c->nee_val + ((step - 1) & 1) * per : nullptr;
+  }
   if (fr) {
     a.partial = fr->part;
     a.red_blocks = 8;
@@ -474,7 +494,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   r.c_hi = hi;
   r.c_lo2 = lo2;
   r.c_hi2 = hi2;
-  std::vector<int> chunks, cells;
+  std::vector<int> chunks, cells, cells_in_chunk_order;
   auto in = [&](int64_t k) { return (k >= lo && k < hi) || (k >= lo2 && k < hi2); };
   // Chunk waves also take the NEE-adjacent cells (nee_chunks) when those mostly share their
   // 4-cell group with other fluid cells -- the pipe's rows along y, vessel trees: each such
@@ -511,6 +531,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   };
   scan(lo, hi);
   if (hi2 > lo2) scan(lo2, hi2);
+  cells_in_chunk_order = cells;
   r.nchunks = (int)chunks.size();
   r.chunk0 = chunks.empty() ? -1 : chunks[0];
   for (size_t i = 1; i < chunks.size() && r.chunk0 >= 0; ++i)
@@ -792,6 +813,47 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     r.nee_fix = true;
     r.nee_blocks = 0;
   }
+  // NEE records where the chunk waves run over a chunk list of the dense box and every chunk
+  // holds at most kNeeRecMax NEE-adjacent cells of at most kNeeRecDirs NEE directions (the pipe
+  // along y: one per chunk); k_nee_fix elsewhere
+  if (r.nee_fix && !cv && !r.groups && !r.lane_masks && !r.stride && r.nchunks > 0 && g_tune[LBM_TUNE_NEE_FIX] == 0) {
+    const std::vector<int>& co = cells_in_chunk_order;
+    std::vector<int> base(r.nchunks + 1), pos(co.size());
+    std::vector<uint32_t> nlv(co.size());
+    bool ok = true;
+    size_t k = 0;
+    for (int i = 0; i < r.nchunks && ok; ++i) {
+      base[i] = (int)k;
+      while (k < co.size() && co[k] / kChunk == chunks[i]) {
+        pos[k] = co[k] % kChunk;
+        nlv[k] = nl_of(co[k]);
+        ok &= __builtin_popcount(nlv[k]) <= kNeeRecDirs;
+        ++k;
+      }
+      ok &= (int)k - base[i] <= kNeeRecMax;
+    }
+    base[r.nchunks] = (int)k;
+    if (ok && k == co.size()) {
+      DevScratch dc, dp, dn;
+      int* pc = nullptr;
+      int* pp = nullptr;
+      uint32_t* pn = nullptr;
+      RCK(upload(c, &pc, co));
+      dc.p = pc;
+      RCK(upload(c, &pp, pos));
+      dp.p = pp;
+      RCK(upload(c, &pn, nlv));
+      dn.p = pn;
+      RCK(upload(c, &r.nee_rec_base, base));
+      r.n_rec = (int)co.size();
+      HIPCK(c, hipMalloc(&r.nee_rec, sizeof(float4) * kNeeRecF4 * r.n_rec));
+      HIPCK(c, launch_nee_records(pc, pp, pn, c->rho, c->ux, c->uy, c->uz, r.nee_rec, r.n_rec, c->L.pitch, c->L.plane,
+                                  c->L.swap, c->s_comp));
+      HIPCK(c, hipStreamSynchronize(c->s_comp));
+      r.nee_records = true;
+      r.nee_fix = false;
+    }
+  }
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }
@@ -806,6 +868,8 @@ void free_range(Range& r) {
   if (r.group_row) (void)hipFree(r.group_row);
   if (r.cell_row) (void)hipFree(r.cell_row);
   if (r.cell_nl) (void)hipFree(r.cell_nl);
+  if (r.nee_rec_base) (void)hipFree(r.nee_rec_base);
+  if (r.nee_rec) (void)hipFree(r.nee_rec);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
 }
@@ -867,6 +931,28 @@ int reset_state(lbm_ctx* c) {
   c->halo_primed = false;
   c->macros_stale = false;
   c->walls_stale = false;
+  c->nee_stale = false;
+  return LBM_OK;
+}
+
+// The NEE cells' slots a run of NEE-record steps left unwritten (lbm_ctx::nee_stale), from the
+// records, before anything reads them as the producer side stores them: buf[cur], the next
+// step's source, gets the values of the last step (k - 1); buf[cur ^ 1], the last step's source
+// (the lazy macros), those of step k - 2 -- except after a single step, whose source holds the raw
+// initial slots step 0 pulls.
+int materialize_nee(lbm_ctx* c) {
+  if (!c->nee_stale) return LBM_OK;
+  const Range& r = c->whole;
+  const int64_t per = (int64_t)r.n_rec * 8;
+  const int k = c->steps_done;
+  if (k >= 1)
+    HIPCK(c, launch_nee_materialize(c->buf[c->cur], r.nee_rec, c->nee_val + ((k - 1) & 1) * per, r.n_rec, c->L.pitch,
+                                    c->L.plane, c->L.swap, 1, c->s_comp));
+  if (k >= 2)
+    HIPCK(c, launch_nee_materialize(c->buf[c->cur ^ 1], r.nee_rec, c->nee_val + ((k - 2) & 1) * per, r.n_rec,
+                                    c->L.pitch, c->L.plane, c->L.swap, 1, c->s_comp));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  c->nee_stale = false;
   return LBM_OK;
 }
 
@@ -1124,7 +1210,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 1, 16};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 2, 16};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
@@ -1394,6 +1480,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       c->red_n = c->whole.npart + 8;
       CK(hipMalloc(&c->red_part, sizeof(double) * 2 * c->red_n));
     }
+    if (c->whole.nee_records) CK(hipMalloc(&c->nee_val, sizeof(float) * 2 * 8 * (size_t)c->whole.n_rec));
     if (c->whole.nee_fix) {  // per (compact) cell: only the NEE-adjacent cells' entries are used
       const int64_t n = c->compact ? c->ncell_c : L.ncell;
       CK(hipMalloc(&c->nee_mac, sizeof(float4) * n));
@@ -1429,6 +1516,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->nee_mac) (void)hipFree(c->nee_mac);
+  if (c->nee_val) (void)hipFree(c->nee_val);
   for (float* p : {c->alloc[0], c->alloc[1], c->rho, c->ux, c->uy, c->uz, c->hist, c->send_up, c->send_dn,
                    c->recv_up, c->recv_dn})
     if (p) (void)hipFree(p);
@@ -1728,6 +1816,7 @@ int rccl_exchange(lbm_ctx* c, int b, bool all, hipEvent_t* halo_end = nullptr, b
 int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
   if (c->bb_pull()) c->walls_stale = true;  // the whole-domain steps below store no wall slots
   else RCK(prime_walls(c));
+  if (c->whole.nee_records && nsteps > 0) c->nee_stale = true;  // ... nor NEE slots (NEE records)
   if (c->sum_mode == LBM_SUM_CUB_TREE) {
     // the reference's order: per step calc_vel_square's terms into reference storage order, then
     // thrust::reduce's CUB tree in fp32 (ldc.cu:660-668)
@@ -1744,6 +1833,10 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
         src = dense;
       }
       const uint32_t* bbl = (c->bb_pull() && !c->bb_raw(k)) ? c->links : nullptr;
+      if (c->whole.nee_records && k >= 1)  // the step's source with its NEE slots (the records of step k - 1)
+        HIPCK(c, launch_nee_materialize(c->buf[c->cur], c->whole.nee_rec,
+                                        c->nee_val + (int64_t)((k - 1) & 1) * c->whole.n_rec * 8, c->whole.n_rec,
+                                        L.pitch, L.plane, L.swap, 1, c->s_comp));
       HIPCK(c, launch_vel_terms(src, c->type, bbl, c->ref_idx, c->terms, L.plane, (L.nz + 1) * L.plane, L.pitch,
                                 L.plane, L.swap, c->s_comp));
       c->cur ^= 1;
@@ -1890,6 +1983,7 @@ int refresh_macros(lbm_ctx* c) {
   const Layout& L = c->L;
   const float* src = c->buf[c->cur ^ 1];  // the last step's source buffer
   if (!c->bb_pull()) RCK(prime_walls(c));  // a producer-side read-out pulls the wall slots
+  RCK(materialize_nee(c));                  // ... and every read-out the NEE slots
   // the last step ran from this buffer: step h.k - 1
   const bool consumer = c->bb_pull() && !c->bb_raw(h.k - 1);
   if (c->compact)  // straight from the compact buffer, addressed as the step kernels address it
@@ -2025,6 +2119,7 @@ int lbm_get_geo(lbm_ctx* c, int8_t* geo) {
 int lbm_get_f(lbm_ctx* c, float* f) {
   if (!c || !f) return LBM_ERR_ARG;
   RCK(lbm_sync(c));
+  RCK(materialize_nee(c));  // the NEE cells' slots as the producer side holds them
   const Layout& L = c->L;
   if (c->compact) {
     // the compact buffer as it is, placed on the host through cmap (no dense device copy); cells
@@ -2081,6 +2176,7 @@ constexpr size_t kCkptSlice = (size_t)64 << 20;  // bytes staged through the hos
 int lbm_checkpoint_save(lbm_ctx* c, const char* path) {
   if (!c || !path) return LBM_ERR_ARG;
   RCK(lbm_sync(c));
+  RCK(materialize_nee(c));  // files hold the NEE values in the NEE cells' slots, whatever the mode
   CkptHeader h{};
   std::memcpy(h.magic, "LBMCKPT1", 8);
   h.version = kCkptVersion;
@@ -2197,6 +2293,14 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
   // them now (its next step pulls them), a consumer-side one never reads them
   c->walls_stale = h.walls_stale != 0;
   if (!c->bb_pull()) RCK(prime_walls(c));
+  // NEE records: the next step takes the values of step k - 1 from its source buffer's NEE slots
+  c->nee_stale = false;
+  if (c->whole.nee_records && c->steps_done >= 1) {
+    HIPCK(c, launch_nee_materialize(c->buf[c->cur], c->whole.nee_rec,
+                                    c->nee_val + (int64_t)((c->steps_done - 1) & 1) * c->whole.n_rec * 8,
+                                    c->whole.n_rec, c->L.pitch, c->L.plane, c->L.swap, 0, c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+  }
   return LBM_OK;
 }
 
@@ -2417,6 +2521,7 @@ int lbm_attach_rccl(lbm_ctx* c, const uint8_t id_bytes[128], int rank, int nrank
   // step computes the macros producer-side from the last step's source: both buffers get them
   // once from the current state, as the producers would have stored them (prime_walls)
   RCK(prime_walls(c));
+  RCK(materialize_nee(c));  // the slab sequence stores and pulls the NEE slots producer-side
   NCCK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
   c->nranks = nranks;
@@ -2485,7 +2590,7 @@ extern "C" int lbm_group_step(lbm_ctx** cs, int n, int nsteps, float* residual_h
     RCK(ensure_halo_buffers(cs[i]));
     // the slab ranges bounce back on the producer side: a context that stepped its whole domain
     // consumer-side first gets its wall slots back
-    if (prime_walls(cs[i]) != LBM_OK) {
+    if (prime_walls(cs[i]) != LBM_OK || materialize_nee(cs[i]) != LBM_OK) {
       c0->err = cs[i]->err;
       return LBM_ERR_HIP;
     }

@@ -612,6 +612,60 @@ __device__ __forceinline__ BoxCell box_cell(const MainArgs& a, int64_t c) {
   return b;
 }
 
+// ---- NEE records (MainArgs::nee_rec; single-domain chunk ranges whose chunk waves collide the
+// NEE-adjacent cells) -------------------------------------------------------------------------
+// boundary_stream writes slot q of NEE cell B = c - e_q from c's post-collision f_q and (rho, u)
+// of the step (ldc.cu:391-456, Poiseulle.cu:748-891), and only c pulls it, at the next step.  So
+// the chunk wave that collides c computes those values right after its relaxation and stores them
+// -- one 32-B record per cell, contiguous per chunk -- and the wave that collides c next step puts
+// them into its pulled populations in place of B's slots.  No scattered 4-B store into B's slots
+// (six of the thirteen microseconds the NEE work cost the pipe, profiles/r05_nee_cost_ab.log), no
+// second collision of c, no launch after the step.  The static part of each record (LDS by DMA
+// beside the pulls): the cell's position in its chunk, its NEE-link mask and the boundary data of
+// its first kNeeRecDirs NEE directions.
+// a component of f4 by a wave-uniform index
+__device__ __forceinline__ float comp4(const f4 v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
+__device__ __forceinline__ f4 with_comp4(f4 v, int j, float x) {
+  return f4{j == 0 ? x : v.x, j == 1 ? x : v.y, j == 2 ? x : v.z, j == 3 ? x : v.w};
+}
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+// next step: the recorded NEE values replace the pulled slots of the cell (lane L, cell j)
+template <int Q>
+__device__ __forceinline__ void nee_rec_sub(f4* v, int lane, int L, int j, uint32_t nl, const float* vals) {
+  if constexpr (Q > 0) {
+    if (nl & (1u << Q)) {  // wave-uniform
+      const float x = vals[__builtin_popcount(nl & ((1u << Q) - 1u))];
+      if (lane == L) v[Q] = with_comp4(v[Q], j, x);
+    }
+  }
+}
+template <int... Qs>
+__device__ __forceinline__ void nee_rec_sub_all(f4* v, int lane, int L, int j, uint32_t nl, const float* vals,
+                                                std::integer_sequence<int, Qs...>) {
+  (nee_rec_sub<Qs>(v, lane, L, j, nl, vals), ...);
+}
+// this step: lane kk collects the value of the cell's kk-th NEE direction
+template <int Q>
+__device__ __forceinline__ void nee_rec_make(const f4* v, int lane, int L, int j, uint32_t nl, const float4* bc, float r,
+                                             float ux, float uy, float uz, const Pref& pre, float omc, float& mine) {
+  if constexpr (Q > 0) {
+    if (nl & (1u << Q)) {  // wave-uniform
+      const int kk = __builtin_popcount(nl & ((1u << Q) - 1u));
+      const float fq = readlane_f(comp4(v[Q], j), L);
+      const float x = nee_value<Q>(fq, bc[kk], r, ux, uy, uz, omc, pre.template of<Q>());
+      if (lane == kk) mine = x;
+    }
+  }
+}
+template <int... Qs>
+__device__ __forceinline__ void nee_rec_make_all(const f4* v, int lane, int L, int j, uint32_t nl, const float4* bc,
+                                                 float r, float ux, float uy, float uz, const Pref& pre, float omc,
+                                                 float& mine, std::integer_sequence<int, Qs...>) {
+  (nee_rec_make<Qs>(v, lane, L, j, nl, bc, r, ux, uy, uz, pre, omc, mine), ...);
+}
+
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
 //        branch) the exact division, counted in exact_waves.  Both paths cost 210-218 VGPRs
@@ -621,14 +675,25 @@ __device__ __forceinline__ BoxCell box_cell(const MainArgs& a, int64_t c) {
 //        entry's type byte and link masks, then the pulls (Rows).
 //  BOX (chunk lists of the device-generated cavity): type bytes and wall links from the cells'
 //        coordinates (box_cell), no loads.
-template <bool FAST, bool SW, bool MASK, bool GROUPS = false, bool COMPACT = false, bool BOX = false>
-__device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask) {
+//  REC (chunk lists of the dense box): NEE records (MainArgs::nee_rec); ridx, the wave's chunk-list
+//        entry, indexes MainArgs::nee_rec_base.  A separate instance: the records' code costs the
+//        instances without it registers
+template <bool FAST, bool SW, bool MASK, bool GROUPS = false, bool COMPACT = false, bool BOX = false, bool REC = false>
+__device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask,
+                                                int ridx = -1) {
+  static_assert(!REC || !(GROUPS || BOX), "NEE records run over the dense box's chunk lists");
   static_assert(GROUPS || !COMPACT, "compact rows run over group lists");
   static_assert(!(BOX && (GROUPS || SW)), "the cavity runs over x-row chunk lists");
   double acc = 0.0;
   int64_t c;
   bool need, take_lo, take_hi;
   f4 v[kQ];
+  int rb = 0, rn = 0;  // NEE records of the chunk: first index, count
+  float4* NL = nullptr;  // this wave's LDS for them: static records, the previous step's values, (rho, u)
+  if constexpr (REC) {
+    __shared__ float4 nee_lds[kBlock / 64][kNeeRecMax * (kNeeRecF4 + 3)];
+    NL = nee_lds[threadIdx.x >> 6];
+  }
   RowsRef ad{};  // COMPACT: the lane's cell and row (Rows again for the bounce-back stores)
   constexpr unsigned kWall4 = kWallAdj * 0x01010101u, kNee4 = kNeeAdj * 0x01010101u;
   uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
@@ -692,7 +757,32 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     need = MASK ? ((lane_mask >> lane) & 1u) != 0 : true;
     take_lo = lane == 0;
     take_hi = lane == 63;
+    // NEE records of the chunk's NEE-adjacent cells: static part and the previous step's values
+    // to LDS by DMA, beside the pulls (nothing in VGPRs while in flight)
+    if (REC) {
+      rb = a.nee_rec_base[ridx];
+      rn = a.nee_rec_base[ridx + 1] - rb;
+    }
+    if (REC && rn > 0) {  // wave-uniform
+      if (lane < rn * kNeeRecF4)
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.nee_rec + (int64_t)rb * kNeeRecF4 + lane), (lds_ptr_t)NL, 16, 0, 0);
+      if (a.nee_in != nullptr && lane < rn * 2)
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.nee_in + ((int64_t)rb * 2 + lane) * 4),
+                                         (lds_ptr_t)(NL + kNeeRecMax * kNeeRecF4), 16, 0, 0);
+    }
     pull4_all<SW>(v, a.src, cb, cb + kChunk, c, take_lo, take_hi, a.pitch, a.plane, need, AllQ{});
+    if (REC && rn > 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes are in
+      if (a.nee_in != nullptr) {
+        const float* vals = reinterpret_cast<const float*>(NL + kNeeRecMax * kNeeRecF4);
+        for (int k = 0; k < rn; ++k) {
+          const int4 h = *reinterpret_cast<const int4*>(NL + k * kNeeRecF4);
+          const int pos = __builtin_amdgcn_readfirstlane(h.x);
+          const uint32_t nl = (uint32_t)__builtin_amdgcn_readfirstlane(h.y);
+          nee_rec_sub_all(v, lane, pos >> 2, pos & 3, nl, vals + k * 8, AllQ{});
+        }
+      }
+    }
   }
   if constexpr (BOX) {
     const BoxCell b0 = box_cell(a, c), b1 = box_cell(a, c + 1), b2 = box_cell(a, c + 2), b3 = box_cell(a, c + 3);
@@ -774,6 +864,19 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   const bool lane_in = (c >= a.c_lo && c + 4 <= a.c_hi) || (c >= a.c_lo2 && c + 4 <= a.c_hi2);
   const bool keep_others = special != 0u || !lane_in || (!a.nee_chunks && (t4 & kNee4));
   const bool whole = store == 0xfu || (store != 0u && !keep_others);
+  if (REC && rn > 0) {  // wave-uniform: the NEE-adjacent cells' (rho, u) to LDS, so that the
+                        // moments need not live through the relaxation
+    const f4 R{r0, r1, r2, r3};
+    float4* M = NL + kNeeRecMax * (kNeeRecF4 + 2);
+    for (int k = 0; k < rn; ++k) {
+      const int4 h = *reinterpret_cast<const int4*>(NL + k * kNeeRecF4);
+      const int pos = __builtin_amdgcn_readfirstlane(h.x);
+      const int L = pos >> 2, j = pos & 3;
+      const float4 m = make_float4(readlane_f(comp4(R, j), L), readlane_f(comp4(UX, j), L),
+                                   readlane_f(comp4(UY, j), L), readlane_f(comp4(UZ, j), L));
+      if (lane == 0) M[k] = m;
+    }
+  }
   if (FAST && fast_wave) {
     relax_cell<0, true>(v, a.tau, a.tau_rcp, r0, x0, y0, z0, AllQ{});
     relax_cell<1, true>(v, a.tau, a.tau_rcp, r1, x1, y1, z1, AllQ{});
@@ -807,6 +910,20 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     if (store & 2u) bb_store_cell<1, SW>(a.dst, bad, m1, v);
     if (store & 4u) bb_store_cell<2, SW>(a.dst, bad, m2, v);
     if (store & 8u) bb_store_cell<3, SW>(a.dst, bad, m3, v);
+  }
+  if (REC && rn > 0) {  // wave-uniform: this step's NEE values of the chunk's NEE-adjacent cells
+    const float4* M = NL + kNeeRecMax * (kNeeRecF4 + 2);
+    for (int k = 0; k < rn; ++k) {
+      const int4 h = *reinterpret_cast<const int4*>(NL + k * kNeeRecF4);
+      const int pos = __builtin_amdgcn_readfirstlane(h.x);
+      const uint32_t nl = (uint32_t)__builtin_amdgcn_readfirstlane(h.y);
+      const int L = pos >> 2, j = pos & 3;
+      const float4 m = M[k];
+      const float r = readlane_f(m.x, 0), ux = readlane_f(m.y, 0), uy = readlane_f(m.z, 0), uz = readlane_f(m.w, 0);
+      float mine = 0.f;
+      nee_rec_make_all(v, lane, L, j, nl, NL + k * kNeeRecF4 + 1, r, ux, uy, uz, Pref::exact(r), a.omc, mine, AllQ{});
+      if (lane < __builtin_popcount(nl)) a.nee_out[(int64_t)(rb + k) * 8 + lane] = mine;
+    }
   }
   float* d = a.dst + aidx(c, 0);
   if (whole) {
@@ -1198,7 +1315,7 @@ __device__ __forceinline__ int64_t chunk_of(const MainArgs& a, int idx) {
 }
 
 template <bool FAST, bool QUARTER, bool SW, bool MASK = false, bool STRIDE = false, bool GROUPS = false,
-          bool COMPACT = false, bool BOX = false, int WPB = kBlock / 64>
+          bool COMPACT = false, bool BOX = false, int WPB = kBlock / 64, bool REC = false>
 __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefronts per workgroup
   __shared__ double red[WPB];
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step is a no-op
@@ -1272,7 +1389,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
       }
     } else if (idx < a.nchunks) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
-      acc = process_chunk<FAST, SW, MASK, false, false, BOX>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base
+      acc = process_chunk<FAST, SW, MASK, false, false, BOX, REC>(a, chunk_of(a, idx) * kChunk, lane, lm, idx);  // uniform base
     }
     slot += a.red_blocks + a.nee_blocks;
   } else {  // dispatched first: their scattered, latency-bound work hides under the chunks
@@ -1291,9 +1408,9 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
 // instance runs one); MASK: the range has lane masks (sparse chunk lists); COMPACT: compact
 // rows (group lists only)
 template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = false, bool COMPACT = false,
-          bool BOX = false>
+          bool BOX = false, bool REC = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(const MainArgs a) {
-  step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT, BOX>(a);
+  step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT, BOX, kBlock / 64, REC>(a);
 }
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
 template <bool SW, bool GROUPS = false, bool STRIDE = false, bool COMPACT = false, bool BOX = false>
@@ -1997,6 +2114,12 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
       if (a.fast_div) k = sw ? k_step<true, true, false, false, true> : k_step<true, false, false, false, true>;
       else k = sw ? k_step<false, true, false, false, true> : k_step<false, false, false, false, true>;
     }
+  } else if (a.nee_rec_base) {  // NEE records (no lane masks, no loop: lbm_ctx's build_range)
+    if (a.chunk_stride || a.lane_masks) return hipErrorInvalidValue;
+    if (a.fast_div) k = sw ? k_step<true, true, false, false, false, false, false, true>
+                           : k_step<true, false, false, false, false, false, false, true>;
+    else k = sw ? k_step<false, true, false, false, false, false, false, true>
+                : k_step<false, false, false, false, false, false, false, true>;
   } else if (a.fast_div) {
     if (a.chunk_stride) k = sw ? k_step<true, true, true, true> : k_step<true, false, true, true>;
     else if (a.lane_masks) k = sw ? k_step<true, true, true> : k_step<true, false, true>;
@@ -2176,6 +2299,69 @@ __global__ void k_nee_gather(const int* __restrict__ cells, const uint32_t* __re
     }
     out[(int64_t)i * kNeeSlots + j] = v;
   }
+}
+
+// NEE records (MainArgs::nee_rec): head {position in the chunk, NEE-link mask, cell, 0}, then the
+// boundary data of the first kNeeRecDirs NEE directions (k_nee_gather's order)
+template <bool SW>
+__global__ void k_nee_records(const int* __restrict__ cells, const int* __restrict__ pos,
+                              const uint32_t* __restrict__ nl, const float* __restrict__ rho,
+                              const float* __restrict__ ux, const float* __restrict__ uy,
+                              const float* __restrict__ uz, float4* __restrict__ rec, int n, int pitch,
+                              int64_t plane) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = cells[i];
+  uint32_t rest = nl[i];
+  float4* r = rec + (int64_t)i * kNeeRecF4;
+  r[0] = make_float4(__int_as_float(pos[i]), __int_as_float((int)rest), __int_as_float((int)c), 0.f);
+  for (int j = 0; j < kNeeRecDirs; ++j) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rest) {
+      const int q = __builtin_ctz(rest);
+      rest &= rest - 1u;
+      const int64_t b = c - cell_off_rt<SW>(q, pitch, plane);
+      v = make_float4(rho[b], ux[b], uy[b], uz[b]);
+    }
+    r[1 + j] = v;
+  }
+}
+// the records' NEE values into their NEE cells' slots of f (the producer-side state: slot q of
+// B = c - e_q), or back
+template <bool SW>
+__global__ void k_nee_materialize(float* __restrict__ f, const float4* __restrict__ rec, float* __restrict__ vals,
+                                  int n, int pitch, int64_t plane, int to_buffer) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 h = rec[(int64_t)i * kNeeRecF4];
+  uint32_t rest = (uint32_t)__float_as_int(h.y);
+  const int64_t c = __float_as_int(h.z);
+  for (int k = 0; rest; ++k) {
+    const int q = __builtin_ctz(rest);
+    rest &= rest - 1u;
+    const int64_t at = aidx(c - cell_off_rt<SW>(q, pitch, plane), q);
+    if (to_buffer) f[at] = vals[(int64_t)i * 8 + k];
+    else vals[(int64_t)i * 8 + k] = f[at];
+  }
+}
+
+hipError_t launch_nee_records(const int* cells, const int* pos, const uint32_t* nl, const float* rho, const float* ux,
+                              const float* uy, const float* uz, float4* rec, int n, int pitch, int64_t plane, int swap,
+                              hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g((n + 255) / 256);
+  if (swap) hipLaunchKernelGGL(k_nee_records<true>, g, dim3(256), 0, s, cells, pos, nl, rho, ux, uy, uz, rec, n, pitch, plane);
+  else hipLaunchKernelGGL(k_nee_records<false>, g, dim3(256), 0, s, cells, pos, nl, rho, ux, uy, uz, rec, n, pitch, plane);
+  return hipGetLastError();
+}
+
+hipError_t launch_nee_materialize(float* f, const float4* rec, float* vals, int n, int pitch, int64_t plane, int swap,
+                                  int to_buffer, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 g((n + 255) / 256);
+  if (swap) hipLaunchKernelGGL(k_nee_materialize<true>, g, dim3(256), 0, s, f, rec, vals, n, pitch, plane, to_buffer);
+  else hipLaunchKernelGGL(k_nee_materialize<false>, g, dim3(256), 0, s, f, rec, vals, n, pitch, plane, to_buffer);
+  return hipGetLastError();
 }
 
 hipError_t launch_bc_uniform(const uint8_t* type, const float* rho, const float* ux, const float* uy,

@@ -122,6 +122,16 @@ struct MainArgs {
                             // own and bounce-back slots, |u|); the NEE blocks add only the NEE values
   int nee_blocks;           // multiple of 8 (keeps the chunk blocks' XCD order)
   int nee_waves;            // active waves per NEE block (1 for short, scattered lists)
+  // NEE records (nullable; single-domain chunk-list ranges whose chunk waves collide the NEE-
+  // adjacent cells, LBM_TUNE_NEE_FIX 0): per chunk-list entry i the records nee_rec_base[i] ..
+  // nee_rec_base[i + 1] - 1 (at most kNeeRecMax); record k: kNeeRecF4 float4 -- {position in the
+  // chunk, NEE-link mask, cell, 0} as ints, then the boundary data of its first kNeeRecDirs NEE
+  // directions; nee_in (null at step 0: B's slots are pulled raw) / nee_out: 8 floats per record,
+  // the NEE values of the previous / this step in the mask's bit order
+  const int* nee_rec_base;
+  const float4* nee_rec;
+  const float* nee_in;
+  float* nee_out;
   float4* nee_mac;          // nullable (single-domain nee_chunks ranges, LBM_TUNE_NEE_FIX): the chunk
                             // waves store each NEE-adjacent cell's (rho, ux, uy, uz) here, indexed by
                             // cell; k_nee_fix (launch_nee_fix, after the step launch) reads them with
@@ -185,7 +195,19 @@ struct ConvState {      // device-resident reference main-loop state (ldc.cu:613
   int nonfinite_k;      // first step whose |u| sum was not finite (0: none)
 };
 
+constexpr int kNeeRecMax = 8;    // NEE records per chunk (ranges with more use k_nee_fix)
+constexpr int kNeeRecDirs = 8;   // NEE directions per record (cells with more: k_nee_fix)
+constexpr int kNeeRecF4 = 1 + kNeeRecDirs;
 hipError_t launch_step(const MainArgs& a, hipStream_t s);
+// NEE records set-up: rec[i] for cells[i] (chunk-relative position pos[i], NEE-link mask nl[i]),
+// boundary data gathered from the NEE cells' macro arrays
+hipError_t launch_nee_records(const int* cells, const int* pos, const uint32_t* nl, const float* rho, const float* ux,
+                              const float* uy, const float* uz, float4* rec, int n, int pitch, int64_t plane, int swap,
+                              hipStream_t s);
+// the NEE values of records vals (8 floats each) into their NEE cells' slots of buffer f
+// (to_buffer = 1), or back from those slots into vals (0)
+hipError_t launch_nee_materialize(float* f, const float4* rec, float* vals, int n, int pitch, int64_t plane, int swap,
+                                  int to_buffer, hipStream_t s);
 // after launch_step of a range with nee_mac: one thread per NEE-adjacent cell (cells, cell_nl,
 // nee_bc, n_nee) stores its NEE neighbours' slots of dst
 hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s);

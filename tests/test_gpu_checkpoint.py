@@ -278,3 +278,31 @@ def test_group_step_after_consumer_side_steps(gpu):
     _same(a.macros(), b.macros(), "macros after the loopback steps")
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (0, 2)], ids=["rec_rec", "rec_blocks", "blocks_rec", "rec_fix"])
+def test_resume_nee_records(gpu, tmp_path, knob, modes):
+    """A pipe whose NEE values travel as NEE records (LBM_TUNE_NEE_FIX 0: the NEE cells' slots are
+    never written while stepping): the file holds the values in those slots (save puts them
+    there), so it resumes bit for bit in a context of any NEE mode, and a records context takes
+    its next step's values back from the loaded slots."""
+    from lbm_amd import cases
+    import lbm_amd
+    knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)
+
+    def make(mode):
+        with lbm_amd.tuned(lbm_amd.TUNE_NEE_FIX, mode):
+            return cases.poiseuille(20, 512, 18)[0]
+
+    a = make(modes[0])
+    a.step(9)
+    path = str(tmp_path / "ck.bin")
+    a.checkpoint_save(path)
+    b = make(modes[1])
+    b.checkpoint_load(path)
+    _same(a.macros(), b.macros(), "macros right after the load")
+    ha, hb = a.step(21), b.step(21)
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32)), "residual histories differ"
+    _same(a.macros(), b.macros(), "macros after 21 more steps")
+    a.close()
+    b.close()

@@ -328,25 +328,47 @@ def test_compact_rows_vs_dense(gpu, knob, case, tmp_path):
 
 @pytest.mark.parametrize("path", ["bif_1cell_compact", "bif_4cell_compact", "ldc_1cell_box"])
 def test_consumer_side_steps_write_no_wall_slot(gpu, knob, path):
-    """With bounce-back on the consumer side no step writes a wall slot: every slot of every wall
-    cell keeps the sentinel it was set to, so no whole-vector or cell-by-cell store of a lane
-    holding a wall strays into it -- the check defined_slots cannot make, since it compares only
-    the slots the modes agree on."""
+    """With bounce-back on the consumer side no wall slot is read, and no step stores into one
+    except where a 4-cell lane stores its whole 16-B vector over a 4-cell group that also holds a
+    fluid cell (the wall cells' slots in that group take the lane's values; nothing reads them).
+    Every other wall slot keeps the sentinel it was set to -- one-cell lanes store cell by cell, so
+    there that is every wall slot -- and so no store of a lane strays into another group or row
+    (the check defined_slots cannot make, since it compares only the slots the modes agree on;
+    ADVICE r04)."""
     from lbm_amd import cases
     import lbm_amd
-    if path == "bif_4cell_compact":
+    four = path == "bif_4cell_compact"
+    if four:
         knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)
         knob(lbm_amd.TUNE_GROUPS, 2)
         knob(lbm_amd.TUNE_COMPACT, 2)
     if path.startswith("bif"):
         lat, geo, _, _ = cases.bifurcation(1)
         assert lat.storage()["compact"]
-        wall, steps = geo == 1, 24
+        fluid, steps = geo == 4, 24
     else:
         lat = cases.ldc_device(32, 32, 32)
         geo = lat.geo()
-        wall, steps = geo == 1, 23  # odd: buffer 1, which lbm_init's bounce-back priming of buffer 0 never touched
-    assert lat.launch_shape()["cells_per_lane"] == (4 if path == "bif_4cell_compact" else 1)
+        fluid, steps = geo == 3, 23  # odd: buffer 1, which the initial bounce-back priming of buffer 0 never touched
+    assert lat.launch_shape()["cells_per_lane"] == (4 if four else 1)
+    wall = geo == 1
+    if four:  # wall cells whose storage group (4 cells along the row, xshift applied) holds no fluid cell
+        lay = lat.layout()
+        ax = 2 if lay["row_axis"] == 1 else 1  # raster axis of the rows: x (2) or y (1)
+        pos = np.arange(geo.shape[ax]) - (lay["x_align"] - 1)
+        grp = np.floor_divide(pos, 4)
+        shape = [1, 1, 1]
+        shape[ax] = -1
+        g = np.broadcast_to(grp.reshape(shape), geo.shape)
+        fl = np.moveaxis(fluid, ax, -1)
+        gg = np.moveaxis(g, ax, -1)
+        has = np.zeros_like(fl)
+        for k in np.unique(grp):
+            sel = gg == k
+            any_fl = (fl & sel).any(axis=-1, keepdims=True)
+            has |= sel & any_fl
+        wall &= ~np.moveaxis(has, -1, ax)
+        assert wall.sum() > 1000
     f = lat.f()
     # distinct small values (the first step of the bifurcation pulls its walls raw)
     sentinel = (0.01 + (np.arange(wall.sum() * 19).reshape(19, -1) % 1021) * 1e-5).astype(np.float32)
@@ -354,7 +376,7 @@ def test_consumer_side_steps_write_no_wall_slot(gpu, knob, path):
     lat.set_f(f)
     lat.step(steps, history=False)
     got = lat.f()[:, wall]
-    assert np.all(np.isfinite(lat.macros()[0][geo == (4 if path.startswith("bif") else 3)]))
+    assert np.all(np.isfinite(lat.macros()[0][fluid]))
     bad = np.count_nonzero(got.view(np.uint32) != sentinel.view(np.uint32))
     assert bad == 0, f"{path}: {bad} wall slots written"
     lat.close()

@@ -45,6 +45,23 @@ PATCHES = {
                    "    if (a2 == 1234.5678f) a.dst[0] = a2;\n"
                    "  }\n"
                    "  return acc;\n}\n\n// ---- one cell per lane")],
+    # wave timestamps (s_memrealtime, 100 MHz): every 4-cell chunk wave of the dense chunk path
+    # records its start and end into g_lab_ts (lbm_lab_ts_copy), values unchanged
+    "wave_ts": [("lbm_kernels.hip",
+                 "      acc = process_chunk<FAST, SW, MASK, false, false, BOX>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base\n    }",
+                 "      const unsigned long long t_in = wall_clock64();\n"
+                 "      acc = process_chunk<FAST, SW, MASK, false, false, BOX>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base\n"
+                 "      if (lane == 0 && idx < (1 << 18)) {\n"
+                 "        g_lab_ts[2 * idx] = t_in;\n"
+                 "        g_lab_ts[2 * idx + 1] = wall_clock64();\n"
+                 "      }\n    }"),
+                ("lbm_kernels.hip", "__device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {",
+                 "__device__ unsigned long long g_lab_ts[2 << 18];\n"
+                 "__device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {"),
+                ("lbm_kernels.hip", "}  // namespace lbm\n",
+                 "}  // namespace lbm\n"
+                 "extern \"C\" int lbm_lab_ts_copy(unsigned long long* out, int n) {\n"
+                 "  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lbm::g_lab_ts), sizeof(unsigned long long) * n);\n}\n")],
 }
 
 
