@@ -67,7 +67,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   // step launch, from those records and the cells' own post-collision slots (cells, cell_nl and
   // nee_bc are its list)
   bool nee_fix = false;
-  // single-domain chunk-list ranges with nee_chunks (LBM_TUNE_NEE_FIX 0): NEE records instead --
+  // single-domain chunk-list ranges with nee_chunks (LBM_TUNE_NEE_FIX 2): NEE records instead --
   // the chunk waves compute the NEE values after their relaxation into lbm_ctx::nee_val and put
   // them into the next step's pulls (MainArgs::nee_rec); per chunk-list entry the first record
   // (nchunks + 1 prefix sums), n_rec records in chunk order
@@ -816,7 +816,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   // NEE records where the chunk waves run over a chunk list of the dense box and every chunk
   // holds at most kNeeRecMax NEE-adjacent cells of at most kNeeRecDirs NEE directions (the pipe
   // along y: one per chunk); k_nee_fix elsewhere
-  if (r.nee_fix && !cv && !r.groups && !r.lane_masks && !r.stride && r.nchunks > 0 && g_tune[LBM_TUNE_NEE_FIX] == 0) {
+  if (r.nee_fix && !cv && !r.groups && !r.lane_masks && !r.stride && r.nchunks > 0 && g_tune[LBM_TUNE_NEE_FIX] == 2) {
     const std::vector<int>& co = cells_in_chunk_order;
     std::vector<int> base(r.nchunks + 1), pos(co.size());
     std::vector<uint32_t> nlv(co.size());

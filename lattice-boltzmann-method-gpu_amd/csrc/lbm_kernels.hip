@@ -764,8 +764,10 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
       rn = a.nee_rec_base[ridx + 1] - rb;
     }
     if (REC && rn > 0) {  // wave-uniform
-      if (lane < rn * kNeeRecF4)
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.nee_rec + (int64_t)rb * kNeeRecF4 + lane), (lds_ptr_t)NL, 16, 0, 0);
+      for (int o = 0; o < rn * kNeeRecF4; o += 64)  // more than one wave-load from 8 records on
+        if (lane + o < rn * kNeeRecF4)
+          __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.nee_rec + (int64_t)rb * kNeeRecF4 + o + lane),
+                                           (lds_ptr_t)(NL + o), 16, 0, 0);
       if (a.nee_in != nullptr && lane < rn * 2)
         __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a.nee_in + ((int64_t)rb * 2 + lane) * 4),
                                          (lds_ptr_t)(NL + kNeeRecMax * kNeeRecF4), 16, 0, 0);

@@ -123,7 +123,7 @@ struct MainArgs {
   int nee_blocks;           // multiple of 8 (keeps the chunk blocks' XCD order)
   int nee_waves;            // active waves per NEE block (1 for short, scattered lists)
   // NEE records (nullable; single-domain chunk-list ranges whose chunk waves collide the NEE-
-  // adjacent cells, LBM_TUNE_NEE_FIX 0): per chunk-list entry i the records nee_rec_base[i] ..
+  // adjacent cells, LBM_TUNE_NEE_FIX 2): per chunk-list entry i the records nee_rec_base[i] ..
   // nee_rec_base[i + 1] - 1 (at most kNeeRecMax); record k: kNeeRecF4 float4 -- {position in the
   // chunk, NEE-link mask, cell, 0} as ints, then the boundary data of its first kNeeRecDirs NEE
   // directions; nee_in (null at step 0: B's slots are pulled raw) / nee_out: 8 floats per record,

@@ -280,9 +280,9 @@ def test_group_step_after_consumer_side_steps(gpu):
     b.close()
 
 
-@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (0, 2)], ids=["rec_rec", "rec_blocks", "blocks_rec", "rec_fix"])
+@pytest.mark.parametrize("modes", [(2, 2), (2, 1), (1, 2), (2, 0)], ids=["rec_rec", "rec_blocks", "blocks_rec", "rec_fix"])
 def test_resume_nee_records(gpu, tmp_path, knob, modes):
-    """A pipe whose NEE values travel as NEE records (LBM_TUNE_NEE_FIX 0: the NEE cells' slots are
+    """A pipe whose NEE values travel as NEE records (LBM_TUNE_NEE_FIX 2: the NEE cells' slots are
     never written while stepping): the file holds the values in those slots (save puts them
     there), so it resumes bit for bit in a context of any NEE mode, and a records context takes
     its next step's values back from the loaded slots."""

@@ -62,6 +62,26 @@ PATCHES = {
                  "}  // namespace lbm\n"
                  "extern \"C\" int lbm_lab_ts_copy(unsigned long long* out, int n) {\n"
                  "  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lbm::g_lab_ts), sizeof(unsigned long long) * n);\n}\n")],
+    # the NEE-record ranges always on the exact-division instance (no FAST body: fewer registers)
+    "rec_exact": [("lbm_kernels.hip", "    if (a.fast_div) k = sw ? k_step<true, true, false, false, false, false, false, true>\n"
+                                      "                           : k_step<true, false, false, false, false, false, false, true>;\n"
+                                      "    else k = sw",
+                   "    k = sw")],
+    # WRONG VALUES (pricing the NEE-record code): without the substitution into the pulls
+    "rec_nosub": [("lbm_kernels.hip", "          nee_rec_sub_all(v, lane, pos >> 2, pos & 3, nl, vals + k * 8, AllQ{});",
+                   "          (void)pos; (void)nl; (void)vals;")],
+    # ... without the production of the values (after the relaxation)
+    "rec_noprod": [("lbm_kernels.hip", "      nee_rec_make_all(v, lane, L, j, nl, NL + k * kNeeRecF4 + 1, r, ux, uy, uz, Pref::exact(r), a.omc, mine, AllQ{});",
+                    "      mine = r + ux + uy + uz + (float)(L + j + (int)nl);")],
+    # ... without the explicit wait for the records' DMA
+    "rec_nowait": [("lbm_kernels.hip", "    if (REC && rn > 0) {\n      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the DMA's LDS writes are in",
+                    "    if (REC && rn > 0) {")],
+    # compact one-cell waves: lanes that are not fluid issue no pulls (exec-masked), values unchanged
+    "c1_mask": [("lbm_kernels.hip", "  pull1_bb<SW>(f, a.src, R, compact_id(c), wl, AllQ{});\n  BcSlots bc{};",
+                 "  if (fluid) pull1_bb<SW>(f, a.src, R, compact_id(c), wl, AllQ{});\n  BcSlots bc{};")],
+    # the one-cell compact pulls as plain (temporal) loads instead of non-temporal ones
+    "c1_temporal": [("lbm_kernels.hip", "  ((f[Qs] = __builtin_nontemporal_load(\n        src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp)",
+                     "  ((f[Qs] = *(\n        src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp)")],
 }
 
 
