@@ -1043,11 +1043,14 @@ __device__ __forceinline__ void pull1_addr(float* f, const float* __restrict__ s
 }
 // the same with bounce-back on the consumer side (MainArgs::bb_pull): where bit q of wl is set
 // (c - e_q a wall), population q comes from the cell's own slot opp(q) -- Poiseulle.cu:601-746's
-// d_dst[q][W] = d_dst[opp q][W + e_q] with W + e_q = c, read where it was stored
+// d_dst[q][W] = d_dst[opp q][W + e_q] with W + e_q = c, read where it was stored.
+// Plain (temporal) loads: the compact lattices' buffers stay in the caches from one step to the
+// next: non-temporal -> plain loads took C4 from 8.13 to 7.75 us per step and the coronary tree
+// from 35.9 to 31.2 us (profiles/r05_c1_temporal_ab.log)
 template <bool SW, class A, class CT, int... Qs>
 __device__ __forceinline__ void pull1_bb(float* f, const float* __restrict__ src, const A& ad, CT c, uint32_t wl,
                                          std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = __builtin_nontemporal_load(
+  ((f[Qs] = *(
         src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp) : fidx(ad.template nb<Qs, SW>(), Qs)))),
    ...);
 }

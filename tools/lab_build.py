@@ -82,6 +82,25 @@ PATCHES = {
     # the one-cell compact pulls as plain (temporal) loads instead of non-temporal ones
     "c1_temporal": [("lbm_kernels.hip", "  ((f[Qs] = __builtin_nontemporal_load(\n        src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp)",
                      "  ((f[Qs] = *(\n        src + ((wl >> Qs) & 1u ? fidx(c, Dir<Qs>::opp)")],
+    # the dense one-cell pulls (k_step1, NEE blocks) as plain loads
+    "t1_dense": [("lbm_kernels.hip", "  ((f[Qs] = __builtin_nontemporal_load(src + fidx(ad.template nb<Qs, SW>(), Qs))), ...);",
+                  "  ((f[Qs] = *(src + fidx(ad.template nb<Qs, SW>(), Qs))), ...);"),
+                 ("lbm_kernels.hip", "  ((f[Qs] = __builtin_nontemporal_load(src + aidx(c - cell_off<Qs, SW>(pitch, plane), Qs))), ...);",
+                  "  ((f[Qs] = *(src + aidx(c - cell_off<Qs, SW>(pitch, plane), Qs))), ...);"),
+                 ("lbm_kernels.hip", "  ((f[Qs] = __builtin_nontemporal_load(base + rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs))), ...);",
+                  "  ((f[Qs] = *(base + rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs))), ...);"),
+                 ("lbm_kernels.hip", "  ((f[Qs] = __builtin_nontemporal_load(\n        base + ((wl >> Qs)",
+                  "  ((f[Qs] = *(\n        base + ((wl >> Qs)")],
+    # the compact 4-cell groups' slice loads as plain loads
+    "t4g_loads": [("lbm_kernels.hip", "  const float* p = need ? src + fidx(s, Q) : src;\n  a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));",
+                   "  const float* p = need ? src + fidx(s, Q) : src;\n  a = *reinterpret_cast<const f4*>(p);")],
+    # the 4-cell group lists' whole 16-B stores as plain stores (chunk lists keep non-temporal ones)
+    "t4g_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
+                    "    for (int q = 0; q < kQ; ++q) {\n      if constexpr (GROUPS) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];\n"
+                    "      else __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));\n    }")],
+    # every 4-cell whole store plain
+    "t4_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
+                   "    for (int q = 0; q < kQ; ++q) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];")],
 }
 
 
