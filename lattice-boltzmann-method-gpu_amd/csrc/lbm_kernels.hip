@@ -226,12 +226,14 @@ __device__ __forceinline__ void pull4_all(f4* v, const float* __restrict__ src, 
 }
 
 // The same for a lane of compact 4-cell groups (GROUPS): the edge floats are the lane's own
-// neighbours, cells slice - 1 (e_x = +1) and slice + 4 (e_x = -1), in the slice's row
+// neighbours, cells slice - 1 (e_x = +1) and slice + 4 (e_x = -1), in the slice's row.  Plain
+// loads here (unlike the chunk lists): C4 x4 138.5 -> 135.1 us (profiles/r05_temporal_ab.log);
+// plain stores were slower (143.5), non-temporal ones stay
 template <int Q, bool SW, class A>
 __device__ __forceinline__ void pull_issue_g(f4& a, float& e, const float* __restrict__ src, const A& ad, bool need) {
   const auto s = ad.template slice<Q, SW>();
   const float* p = need ? src + fidx(s, Q) : src;
-  a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+  a = *reinterpret_cast<const f4*>(p);
   if constexpr (SDir<Q, SW>::x == 1) {
     auto o = fidx(s - 1, Q);
     asm volatile("" : "+v"(o));
@@ -1039,7 +1041,7 @@ __device__ __forceinline__ void fix_store_all(const float* f, float* __restrict_
 template <bool SW, class A, int... Qs>
 __device__ __forceinline__ void pull1_addr(float* f, const float* __restrict__ src, const A& ad,
                                            std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = __builtin_nontemporal_load(src + fidx(ad.template nb<Qs, SW>(), Qs))), ...);
+  ((f[Qs] = *(src + fidx(ad.template nb<Qs, SW>(), Qs))), ...);
 }
 // the same with bounce-back on the consumer side (MainArgs::bb_pull): where bit q of wl is set
 // (c - e_q a wall), population q comes from the cell's own slot opp(q) -- Poiseulle.cu:601-746's
@@ -1057,10 +1059,13 @@ __device__ __forceinline__ void pull1_bb(float* f, const float* __restrict__ src
 
 // One cell per lane (small lattices: a wave per 64 cells, so 4x the waves of the chunk path
 // and a quarter of its per-wave latency): plain pulls, exact division, bounce-back slots.
+// Plain (temporal) loads throughout the one-cell paths: their lattices stay in the caches
+// between steps (LDC 64^3 11.13 -> 9.80 us per step against non-temporal loads,
+// profiles/r05_temporal_ab.log)
 template <bool SW, int... Qs>
 __device__ __forceinline__ void pull1_all(float* f, const float* __restrict__ src, int64_t c, int pitch,
                                           int64_t plane, std::integer_sequence<int, Qs...>) {
-  ((f[Qs] = __builtin_nontemporal_load(src + aidx(c - cell_off<Qs, SW>(pitch, plane), Qs))), ...);
+  ((f[Qs] = *(src + aidx(c - cell_off<Qs, SW>(pitch, plane), Qs))), ...);
 }
 
 // The same pulls for a wave whose cells all lie in chunk ch (lane cell ch * 256 + l): a
@@ -1076,7 +1081,7 @@ __device__ __forceinline__ void pull1w_all(float* f, const float* __restrict__ s
   const int W = (int)((plane + pitch + 1) >> 8) + 2;
   const float* base = src + (ch - W) * (kQ * kChunk);
   const int r0 = l + W * kChunk;
-  ((f[Qs] = __builtin_nontemporal_load(base + rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs))), ...);
+  ((f[Qs] = *(base + rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs))), ...);
 }
 
 // one cell's collision and stores once its pulls, type byte and link masks are in
@@ -1116,7 +1121,7 @@ __device__ __forceinline__ void pull1w_bb(float* f, const float* __restrict__ sr
   const int W = (int)((plane + pitch + 1) >> 8) + 2;
   const float* base = src + (ch - W) * (kQ * kChunk);
   const int r0 = l + W * kChunk;
-  ((f[Qs] = __builtin_nontemporal_load(
+  ((f[Qs] = *(
         base + ((wl >> Qs) & 1u ? rel_aidx(r0, Dir<Qs>::opp) : rel_aidx(r0 - (int)cell_off<Qs, SW>(pitch, plane), Qs)))),
    ...);
 }

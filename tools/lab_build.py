@@ -98,6 +98,9 @@ PATCHES = {
     "t4g_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
                     "    for (int q = 0; q < kQ; ++q) {\n      if constexpr (GROUPS) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];\n"
                     "      else __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));\n    }")],
+    # the one-cell paths' stores non-temporal
+    "t1_ntstores": [("lbm_kernels.hip", "  ((dst[aidx(c, Qs)] = f[Qs]), ...);\n  if (m) {",
+                     "  (__builtin_nontemporal_store(f[Qs], dst + aidx(c, Qs)), ...);\n  if (m) {")],
     # every 4-cell whole store plain
     "t4_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
                    "    for (int q = 0; q < kQ; ++q) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];")],
