@@ -957,8 +957,6 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
         P[3] = make_float4(v[8][j], v[9][j], v[10][j], v[11][j]);
         P[4] = make_float4(v[12][j], v[13][j], v[14][j], v[15][j]);
         P[5] = make_float4(v[16][j], v[17][j], v[18][j], 0.f);
-        P[6] = make_float4(0.f, 0.f, 0.f, 0.f);  // the whole line: no partial-line write
-        P[7] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
   }
   float* d = a.dst + aidx(c, 0);

@@ -134,7 +134,7 @@ struct MainArgs {
   float* nee_out;
   // NEE posts (nullable; single-domain nee_chunks ranges, LBM_TUNE_NEE_FIX 0): the chunk waves
   // write each NEE-adjacent cell's post -- kNeePostF4 float4: (rho, ux, uy, uz), then its 19
-  // post-collision populations and a pad to 128 B -- at list index nee_wbase[w] + the cell's rank among
+  // post-collision populations (and a pad) -- at list index nee_wbase[w] + the cell's rank among
   // the NEE-adjacent cells of entry wave w (a chunk-list entry, or 64 group-list entries; lanes
   // in order, a lane's cells in order); k_nee_fix (launch_nee_fix, after the step launch) reads
   // post i with list entry i and stores the NEE values
@@ -218,9 +218,7 @@ hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s);
 // NEE directions of a cell whose boundary data is loaded ahead (one flat face: 5); a cell
 // with more (edges and corners of several faces) loads the rest where they are used
 constexpr int kNeeSlots = 5;
-// an NEE post: (rho, u), the 19 populations, pad -- one whole 128-B line, written by one wave
-// (96-B posts shared lines between waves, and the chunk waves ran 4.5 us slower on C3)
-constexpr int kNeePostF4 = 8;
+constexpr int kNeePostF4 = 6;  // an NEE post: (rho, u) + 19 populations + pad
 // nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of nl[i]
 // 1 into *differs when some NEE cell's record (rho, ux, uy, uz) differs bitwise from cell ref's
 hipError_t launch_bc_uniform(const uint8_t* type, const float* rho, const float* ux, const float* uy,
