@@ -62,14 +62,11 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   float4* nee_bc = nullptr;     // their first kNeeSlots NEE neighbours' boundary data (static)
   int n_nee = 0, nee_blocks = 0, nee_waves = 4;
   bool nee_chunks = false;  // 4-cell ranges: chunk waves also store the NEE-adjacent cells (MainArgs)
-  // single-domain nee_chunks ranges (LBM_TUNE_NEE_FIX): no NEE blocks; the chunk waves write each
-  // NEE-adjacent cell's NEE post -- its (rho, u) and post-collision populations -- into
-  // lbm_ctx::nee_post, and k_nee_fix stores the NEE values after the step launch from those posts
-  // (cells, cell_nl and nee_bc are its list, in the order the chunk waves meet the cells: post i
-  // belongs to list entry i; nee_wbase: per entry wave -- a chunk-list entry, or 64 group-list
-  // entries -- the list index of its first such cell, n + 1 prefix sums)
+  // single-domain nee_chunks ranges (LBM_TUNE_NEE_FIX): no NEE blocks; the chunk waves record the
+  // NEE-adjacent cells' (rho, u) in lbm_ctx::nee_mac and k_nee_fix stores the NEE values after the
+  // step launch, from those records and the cells' own post-collision slots (cells, cell_nl and
+  // nee_bc are its list)
   bool nee_fix = false;
-  int* nee_wbase = nullptr;
   // single-domain chunk-list ranges with nee_chunks (LBM_TUNE_NEE_FIX 2): NEE records instead --
   // the chunk waves compute the NEE values after their relaxation into lbm_ctx::nee_val and put
   // them into the next step's pulls (MainArgs::nee_rec); per chunk-list entry the first record
@@ -117,7 +114,7 @@ struct lbm_ctx {
   int8_t* codes = nullptr;               // reference codes per storage cell (lbm_get_geo)
   float *bc_in = nullptr, *bc_out = nullptr;  // inlet / outlet u_y tables (lbm_init_case)
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
-  float4* nee_post = nullptr;  // whole.nee_fix: kNeePostF4 per NEE-adjacent cell (Range::nee_fix)
+  float4* nee_mac = nullptr;  // whole.nee_fix: (rho, u) of the NEE-adjacent cells, per (compact) cell
   // whole.nee_records: the NEE values by step parity (2 x n_rec x 8 floats), and whether the NEE
   // cells' slots of the two buffers miss them (steps since the last materialize_nee)
   float* nee_val = nullptr;
@@ -428,8 +425,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.cells = r.cells; a.cell_nl = r.cell_nl; a.nee_bc = r.nee_bc; a.n_nee = r.n_nee;
   a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
   a.nee_chunks = r.nee_chunks ? 1 : 0;
-  a.nee_post = r.nee_fix ? c->nee_post : nullptr;
-  a.nee_wbase = r.nee_fix ? r.nee_wbase : nullptr;
+  a.nee_mac = r.nee_fix ? c->nee_mac : nullptr;
   if (r.nee_records) {
     const int64_t per = (int64_t)r.n_rec * 8;
     a.nee_rec_base = r.nee_rec_base;
@@ -545,7 +541,6 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     HIPCK(c, hipMemcpy(r.chunks, chunks.data(), sizeof(int) * r.nchunks, hipMemcpyHostToDevice));
   }
   bool group1 = false;  // a sparse list too short for the 4-cell path: one-cell group list
-  std::vector<int> gl;  // the group list (group lists only)
   {
     const int cpl = g_tune[LBM_TUNE_CELLS_PER_LANE];  // A/B switch: 1 or 4 (0: by size)
     r.quarter = cpl ? (cpl == 1) : (r.nchunks <= kQuarterMaxChunks);
@@ -582,6 +577,49 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   if (r.quarter) cells.clear();
   // the NEE-link mask of k_flag_fluid: q crosses the NEE neighbour's face (e_q . n == 1)
   auto nl_of = [&](int64_t cell) { return nlk[cell]; };
+  r.n_nee = (int)cells.size();
+  if (r.n_nee) {
+    std::vector<uint32_t> nl(cells.size());
+    for (size_t i = 0; i < cells.size(); ++i) nl[i] = nl_of(cells[i]);
+    // group cells with the same directions (inlet / outlet / lid faces, edges) so that the
+    // lanes of a wave take the same branches; cell order within a group
+    std::vector<size_t> perm(cells.size());
+    for (size_t i = 0; i < perm.size(); ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](size_t x, size_t y) { return nl[x] < nl[y]; });
+    std::vector<int> sc(cells.size());
+    std::vector<uint32_t> snl(cells.size());
+    for (size_t i = 0; i < perm.size(); ++i) {
+      sc[i] = cells[perm[i]];
+      snl[i] = nl[perm[i]];
+    }
+    int64_t adj = 0;  // list neighbours that are storage neighbours (their lanes share lines)
+    for (size_t i = 1; i < sc.size(); ++i) adj += sc[i] == sc[i - 1] + 1;
+    if (sc.size() > 1) contig = (double)adj / (double)(sc.size() - 1);
+    HIPCK(c, hipMalloc(&r.cells, sizeof(int) * r.n_nee));
+    HIPCK(c, hipMemcpy(r.cells, sc.data(), sizeof(int) * r.n_nee, hipMemcpyHostToDevice));
+    HIPCK(c, hipMalloc(&r.cell_nl, sizeof(uint32_t) * r.n_nee));
+    HIPCK(c, hipMemcpy(r.cell_nl, snl.data(), sizeof(uint32_t) * r.n_nee, hipMemcpyHostToDevice));
+    // the boundary cells' data is written by classification and never changes afterwards
+    // (gathered from the dense arrays: compact cells are translated first)
+    HIPCK(c, hipMalloc(&r.nee_bc, sizeof(float4) * kNeeSlots * r.n_nee));
+    DevScratch dense_ids;
+    const int* gather_ids = r.cells;
+    if (cv) {
+      std::vector<int> dsc(sc.size()), rows(sc.size());
+      for (size_t i = 0; i < sc.size(); ++i) {
+        dsc[i] = (*cv->dense_of)[sc[i]];
+        rows[i] = (*cv->row_of)[sc[i] >> 2];
+      }
+      int* p = nullptr;
+      RCK(upload(c, &p, dsc));
+      dense_ids.p = p;
+      gather_ids = p;
+      RCK(upload(c, &r.cell_row, rows));
+    }
+    HIPCK(c, launch_nee_gather(gather_ids, r.cell_nl, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.n_nee, c->L.pitch,
+                               c->L.plane, c->L.swap, c->s_comp));
+    HIPCK(c, hipStreamSynchronize(c->s_comp));
+  }
   // Lane masks for the 4-cell path: bit l of a chunk's mask is set when lane l (cells 4l ..
   // 4l+3) holds a cell the chunk wave updates (fluid, in range, not NEE-adjacent unless
   // nee_chunks) or neighbours
@@ -678,6 +716,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       // coronary tree (59 vs 73 us per step with single groups), and cost the upsampled
       // bifurcation, whose runs are long anyway, 3% (profiles/r03_groups_ab.log)
       const int seg = std::max(1, g_tune[LBM_TUNE_GROUP_SEGMENT]);
+      std::vector<int> gl;
       int64_t cells_in = 0;
       for (int ch : chunks)
         for (int l0 = 0; l0 < 64; l0 += seg) {
@@ -765,85 +804,6 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     const int64_t waves = (int64_t)r.main_blocks * ((cv ? kBlock1c : kBlock) / 64);  // four per SIMD fit
     r.one_round = waves <= (int64_t)cus * 16;
   }
-  // k_nee_fix (LBM_TUNE_NEE_FIX 0, and 2 where NEE records do not apply): the NEE-adjacent cells
-  // in the order the chunk waves meet them -- entry waves in list order, lanes in order, a lane's
-  // cells in order -- so that a wave finds its cells' posts by its entry's base and their ranks
-  // among the wave's such cells
-  const bool fix_mode = single && !r.quarter && r.nee_chunks && !cells.empty() && g_tune[LBM_TUNE_NEE_FIX] != 1;
-  std::vector<int> wbase;
-  if (fix_mode) {
-    auto nee_upd = [&](int64_t k) { return in(k) && (t[k] & kClassMask) == kFluid && (t[k] & kNeeAdj); };
-    std::vector<int> wo;
-    wo.reserve(cells.size());
-    if (r.groups) {
-      const int64_t nw = (r.ngroups + 63) / 64;
-      for (int64_t w = 0; w < nw; ++w) {
-        wbase.push_back((int)wo.size());
-        for (int64_t e = w * 64; e < std::min<int64_t>(r.ngroups, w * 64 + 64); ++e) {
-          if (gl[e] & 1) continue;
-          for (int64_t k = gl[e]; k < gl[e] + 4; ++k)
-            if (nee_upd(k)) wo.push_back((int)k);
-        }
-      }
-    } else {
-      size_t k = 0;
-      for (int i = 0; i < r.nchunks; ++i) {
-        wbase.push_back((int)k);
-        while (k < cells_in_chunk_order.size() && cells_in_chunk_order[k] / kChunk == chunks[i]) ++k;
-      }
-      wo.assign(cells_in_chunk_order.begin(), cells_in_chunk_order.begin() + (long)k);
-    }
-    wbase.push_back((int)wo.size());
-    if (wo.size() != cells.size()) {  // every NEE-adjacent cell of the range lies in an entry wave
-      c->err = "build_range: the NEE posts cover " + std::to_string(wo.size()) + " of " + std::to_string(cells.size()) +
-               " NEE-adjacent cells";
-      return LBM_ERR_GEOMETRY;
-    }
-    cells = wo;
-  }
-  r.n_nee = (int)cells.size();
-  if (r.n_nee) {
-    std::vector<uint32_t> nl(cells.size());
-    for (size_t i = 0; i < cells.size(); ++i) nl[i] = nl_of(cells[i]);
-    // group cells with the same directions (inlet / outlet / lid faces, edges) so that the
-    // lanes of a wave take the same branches; cell order within a group
-    std::vector<size_t> perm(cells.size());
-    for (size_t i = 0; i < perm.size(); ++i) perm[i] = i;
-    if (!fix_mode) std::stable_sort(perm.begin(), perm.end(), [&](size_t x, size_t y) { return nl[x] < nl[y]; });
-    std::vector<int> sc(cells.size());
-    std::vector<uint32_t> snl(cells.size());
-    for (size_t i = 0; i < perm.size(); ++i) {
-      sc[i] = cells[perm[i]];
-      snl[i] = nl[perm[i]];
-    }
-    int64_t adj = 0;  // list neighbours that are storage neighbours (their lanes share lines)
-    for (size_t i = 1; i < sc.size(); ++i) adj += sc[i] == sc[i - 1] + 1;
-    if (sc.size() > 1) contig = (double)adj / (double)(sc.size() - 1);
-    HIPCK(c, hipMalloc(&r.cells, sizeof(int) * r.n_nee));
-    HIPCK(c, hipMemcpy(r.cells, sc.data(), sizeof(int) * r.n_nee, hipMemcpyHostToDevice));
-    HIPCK(c, hipMalloc(&r.cell_nl, sizeof(uint32_t) * r.n_nee));
-    HIPCK(c, hipMemcpy(r.cell_nl, snl.data(), sizeof(uint32_t) * r.n_nee, hipMemcpyHostToDevice));
-    // the boundary cells' data is written by classification and never changes afterwards
-    // (gathered from the dense arrays: compact cells are translated first)
-    HIPCK(c, hipMalloc(&r.nee_bc, sizeof(float4) * kNeeSlots * r.n_nee));
-    DevScratch dense_ids;
-    const int* gather_ids = r.cells;
-    if (cv) {
-      std::vector<int> dsc(sc.size()), rows(sc.size());
-      for (size_t i = 0; i < sc.size(); ++i) {
-        dsc[i] = (*cv->dense_of)[sc[i]];
-        rows[i] = (*cv->row_of)[sc[i] >> 2];
-      }
-      int* p = nullptr;
-      RCK(upload(c, &p, dsc));
-      dense_ids.p = p;
-      gather_ids = p;
-      RCK(upload(c, &r.cell_row, rows));
-    }
-    HIPCK(c, launch_nee_gather(gather_ids, r.cell_nl, c->rho, c->ux, c->uy, c->uz, r.nee_bc, r.n_nee, c->L.pitch,
-                               c->L.plane, c->L.swap, c->s_comp));
-    HIPCK(c, hipStreamSynchronize(c->s_comp));
-  }
   r.nee_waves = nee_waves_for(r.n_nee, contig);
   r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);
   // the single-domain range of a lattice whose chunk waves collide the NEE-adjacent cells: their
@@ -852,7 +812,6 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   if (single && !r.quarter && r.nee_chunks && r.n_nee > 0 && g_tune[LBM_TUNE_NEE_FIX] != 1) {
     r.nee_fix = true;
     r.nee_blocks = 0;
-    if (fix_mode) RCK(upload(c, &r.nee_wbase, wbase));
   }
   // NEE records where the chunk waves run over a chunk list of the dense box and every chunk
   // holds at most kNeeRecMax NEE-adjacent cells of at most kNeeRecDirs NEE directions (the pipe
@@ -910,7 +869,6 @@ void free_range(Range& r) {
   if (r.cell_row) (void)hipFree(r.cell_row);
   if (r.cell_nl) (void)hipFree(r.cell_nl);
   if (r.nee_rec_base) (void)hipFree(r.nee_rec_base);
-  if (r.nee_wbase) (void)hipFree(r.nee_wbase);
   if (r.nee_rec) (void)hipFree(r.nee_rec);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
@@ -1523,7 +1481,10 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       CK(hipMalloc(&c->red_part, sizeof(double) * 2 * c->red_n));
     }
     if (c->whole.nee_records) CK(hipMalloc(&c->nee_val, sizeof(float) * 2 * 8 * (size_t)c->whole.n_rec));
-    if (c->whole.nee_fix) CK(hipMalloc(&c->nee_post, sizeof(float4) * kNeePostF4 * (size_t)c->whole.n_nee));
+    if (c->whole.nee_fix) {  // per (compact) cell: only the NEE-adjacent cells' entries are used
+      const int64_t n = c->compact ? c->ncell_c : L.ncell;
+      CK(hipMalloc(&c->nee_mac, sizeof(float4) * n));
+    }
     c->edge.part = c->whole.part + c->whole.npart;
     c->mid.part = c->edge.part + c->edge.npart;
   }
@@ -1554,7 +1515,7 @@ void lbm_destroy(lbm_ctx* c) {
   if (c->s_comp) (void)hipStreamSynchronize(c->s_comp);
   if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  if (c->nee_post) (void)hipFree(c->nee_post);
+  if (c->nee_mac) (void)hipFree(c->nee_mac);
   if (c->nee_val) (void)hipFree(c->nee_val);
   for (float* p : {c->alloc[0], c->alloc[1], c->rho, c->ux, c->uy, c->uz, c->hist, c->send_up, c->send_dn,
                    c->recv_up, c->recv_dn})

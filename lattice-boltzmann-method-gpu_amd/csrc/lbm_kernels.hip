@@ -668,11 +668,6 @@ __device__ __forceinline__ void nee_rec_make_all(const f4* v, int lane, int L, i
   (nee_rec_make<Qs>(v, lane, L, j, nl, bc, r, ux, uy, uz, pre, omc, mine), ...);
 }
 
-// lanes below this one with their bit set in m
-__device__ __forceinline__ int mbcnt64(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 // One wave's chunk: pull, collide, store; returns the lane's |u| sum.
 //  FAST: the 3-VALU quotient when the whole wave lies in its domain, else (a wave-uniform
 //        branch) the exact division, counted in exact_waves.  Both paths cost 210-218 VGPRs
@@ -682,12 +677,12 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 //        entry's type byte and link masks, then the pulls (Rows).
 //  BOX (chunk lists of the device-generated cavity): type bytes and wall links from the cells'
 //        coordinates (box_cell), no loads.
-//  REC (chunk lists of the dense box): NEE records (MainArgs::nee_rec), indexed through
-//        MainArgs::nee_rec_base by ew.  A separate instance: the records' code costs the
+//  REC (chunk lists of the dense box): NEE records (MainArgs::nee_rec); ridx, the wave's chunk-list
+//        entry, indexes MainArgs::nee_rec_base.  A separate instance: the records' code costs the
 //        instances without it registers
 template <bool FAST, bool SW, bool MASK, bool GROUPS = false, bool COMPACT = false, bool BOX = false, bool REC = false>
 __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, int lane, uint64_t lane_mask,
-                                                int ew = 0) {  // the entry wave: chunk-list entry / 64 group entries
+                                                int ridx = -1) {
   static_assert(!REC || !(GROUPS || BOX), "NEE records run over the dense box's chunk lists");
   static_assert(GROUPS || !COMPACT, "compact rows run over group lists");
   static_assert(!(BOX && (GROUPS || SW)), "the cavity runs over x-row chunk lists");
@@ -767,8 +762,8 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     // NEE records of the chunk's NEE-adjacent cells: static part and the previous step's values
     // to LDS by DMA, beside the pulls (nothing in VGPRs while in flight)
     if (REC) {
-      rb = a.nee_rec_base[ew];
-      rn = a.nee_rec_base[ew + 1] - rb;
+      rb = a.nee_rec_base[ridx];
+      rn = a.nee_rec_base[ridx + 1] - rb;
     }
     if (REC && rn > 0) {  // wave-uniform
       for (int o = 0; o < rn * kNeeRecF4; o += 64)  // more than one wave-load from 8 records on
@@ -844,7 +839,7 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     const int64_t cj = c + j;
     // NEE-adjacent cells belong to the NEE blocks of the launch (nee_cell), unless the range
     // hands the chunk waves their own slots (nee_chunks: the NEE blocks then only add the NEE
-    // neighbours' slots, or, nee_post, k_nee_fix does after the launch)
+    // neighbours' slots, or, nee_mac, k_nee_fix does after the launch)
     const bool in = ((cj >= a.c_lo && cj < a.c_hi) || (cj >= a.c_lo2 && cj < a.c_hi2)) && (t & kClassMask) == kFluid &&
                     (a.nee_chunks || !(t & kNeeAdj));
     if (in) {
@@ -852,26 +847,13 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
       acc += (double)sqrtf(UX[j] * UX[j] + UY[j] * UY[j] + UZ[j] * UZ[j]);
     }
   }
-  // NEE posts for k_nee_fix: the NEE-adjacent cells this wave stores (nst), their (rho, u) now and
-  // their post-collision populations after the relaxation, at list index nee_wbase[ew] + their
-  // rank among the wave's such cells (lanes in order, a lane's cells in order; build_range lists
-  // them the same way)
-  unsigned nst = 0u;
-  int pbase = 0;
-  if (a.nee_post != nullptr) {
+  if (a.nee_mac != nullptr && __any(store != 0u && (t4 & kNee4) != 0u)) {  // wave-uniform
+    // the NEE-adjacent cells' (rho, u) of this step for k_nee_fix (one 16-B store per cell)
+    const f4 R{r0, r1, r2, r3};
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if ((store & (1u << j)) && ((t4 >> (8 * j)) & kNeeAdj)) nst |= 1u << j;
-    if (__any(nst != 0u)) {  // wave-uniform
-      pbase = a.nee_wbase[ew] + mbcnt64(__ballot(nst & 1u)) + mbcnt64(__ballot(nst & 2u)) +
-              mbcnt64(__ballot(nst & 4u)) + mbcnt64(__ballot(nst & 8u));
-      const f4 R{r0, r1, r2, r3};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (nst & (1u << j))
-          a.nee_post[(int64_t)(pbase + __builtin_popcount(nst & ((1u << j) - 1u))) * kNeePostF4] =
-              make_float4(R[j], UX[j], UY[j], UZ[j]);
-    }
+      if ((store & (1u << j)) && ((t4 >> (8 * j)) & kNeeAdj))
+        a.nee_mac[c + j] = make_float4(R[j], UX[j], UY[j], UZ[j]);
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
   // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
@@ -946,18 +928,6 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
       nee_rec_make_all(v, lane, L, j, nl, NL + k * kNeeRecF4 + 1, r, ux, uy, uz, Pref::exact(r), a.omc, mine, AllQ{});
       if (lane < __builtin_popcount(nl)) a.nee_out[(int64_t)(rb + k) * 8 + lane] = mine;
     }
-  }
-  if (a.nee_post != nullptr && __any(nst != 0u)) {  // wave-uniform
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (nst & (1u << j)) {
-        float4* P = a.nee_post + (int64_t)(pbase + __builtin_popcount(nst & ((1u << j) - 1u))) * kNeePostF4;
-        P[1] = make_float4(v[0][j], v[1][j], v[2][j], v[3][j]);
-        P[2] = make_float4(v[4][j], v[5][j], v[6][j], v[7][j]);
-        P[3] = make_float4(v[8][j], v[9][j], v[10][j], v[11][j]);
-        P[4] = make_float4(v[12][j], v[13][j], v[14][j], v[15][j]);
-        P[5] = make_float4(v[16][j], v[17][j], v[18][j], 0.f);
-      }
   }
   float* d = a.dst + aidx(c, 0);
   if (whole) {
@@ -1294,16 +1264,22 @@ __device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {
   return (double)sqrtf(ux * ux + uy * uy + uz * uz);
 }
 
-// NEE values after the step launch (MainArgs::nee_post; single-domain 4-cell ranges whose chunk
-// waves collide the NEE-adjacent cells, nee_chunks): a chunk wave posted each such cell's (rho, u)
-// of the step and its post-collision populations, so one thread per NEE-adjacent cell stores the
-// values boundary_stream writes into its NEE neighbours (ldc.cu:391-456, Poiseulle.cu:748-891,
-// bifurcation.cu:877-1021) -- the same values nee_cell computes, without nee_cell's 19 scattered
-// pulls and its second collision of the cell.  Every load is indexed by the list entry (one
-// round trip; the cell id is needed only for the stores).  The prefactors RN(rho / d) by the
-// exact division: the step's fast quotient is proven equal to it wherever the step used it.
+// NEE values after the step launch (MainArgs::nee_mac; single-domain 4-cell ranges whose chunk
+// waves collide the NEE-adjacent cells, nee_chunks): a chunk wave recorded each such cell's
+// (rho, u) of the step and stored its post-collision populations into its own slots of dst, so
+// one thread per NEE-adjacent cell stores the values boundary_stream writes into its NEE
+// neighbours (ldc.cu:391-456, Poiseulle.cu:748-891, bifurcation.cu:877-1021) -- the same values
+// nee_cell computes, without nee_cell's 19 scattered pulls and its second collision of the cell.
+// The prefactors RN(rho / d) by the exact division: the step's fast quotient is proven equal to
+// it wherever the step used it.
+template <int... Qs>
+__device__ __forceinline__ void own_slots(float* f, const float* __restrict__ dst, int64_t c, uint32_t nl,
+                                          std::integer_sequence<int, Qs...>) {
+  ((f[Qs] = ((nl >> Qs) & 1u) ? dst[fidx(c, Qs)] : 0.0f), ...);
+}
 template <bool SW, bool COMPACT>
 __global__ __launch_bounds__(kBlock) void k_nee_fix(const MainArgs a) {
+  if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step was a no-op
   const int i = blockIdx.x * kBlock + (int)threadIdx.x;
   if (i >= a.n_nee) return;
   const int64_t c = a.cells[i];
@@ -1311,11 +1287,9 @@ __global__ __launch_bounds__(kBlock) void k_nee_fix(const MainArgs a) {
   const float4* rec = a.nee_bc + (int64_t)i * kNeeSlots;
   const BcSlots bc = a.bc_uniform ? BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const}
                                   : BcSlots{rec[0], rec[1], rec[2], rec[3], rec[4]};
-  const float4* P = a.nee_post + (int64_t)i * kNeePostF4;
-  const float4 m = P[0], p1 = P[1], p2 = P[2], p3 = P[3], p4 = P[4], p5 = P[5];
-  if (a.stopped != nullptr && *a.stopped) return;  // converged: the step was a no-op (posts stale)
-  const float f[kQ] = {p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w, p3.x, p3.y,
-                       p3.z, p3.w, p4.x, p4.y, p4.z, p4.w, p5.x, p5.y, p5.z};
+  const float4 m = a.nee_mac[c];
+  float f[kQ];
+  own_slots(f, a.dst, c, nl, AllQ{});
   const Pref pre = Pref::exact(m.x);
   if constexpr (COMPACT) {
     const RowsRef ad{a.rowrec, c, a.cell_row[i]};
@@ -1409,9 +1383,9 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
       const int64_t lo = (b & 7) * per, hi = min(nw, lo + per);
       const int step = (a.main_blocks >> 3) * (WPB);
       for (int64_t i = lo + (b >> 3) * (WPB) + wave; i < hi; i += step)
-        acc += process_chunk<FAST, SW, false, true, COMPACT>(a, i * 64, lane, 0, (int)i);
+        acc += process_chunk<FAST, SW, false, true, COMPACT>(a, i * 64, lane, 0);
     } else if constexpr (GROUPS) {  // compact 4-cell groups: wave idx takes list entries 64 idx ..
-      if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true, COMPACT>(a, (int64_t)idx * 64, lane, 0, idx);
+      if ((int64_t)idx * 64 < a.ngroups) acc = process_chunk<FAST, SW, false, true, COMPACT>(a, (int64_t)idx * 64, lane, 0);
     } else if constexpr (QUARTER) {  // one cell per lane: wave idx takes quarter idx % 4 of chunk idx / 4
       if ((idx >> 2) < a.nchunks)
         acc = process_cell1<SW, BOX>(a, chunk_of(a, idx >> 2), (idx & 3) * 64 + lane);
@@ -1421,7 +1395,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
       const int step = (a.main_blocks >> 3) * (WPB);
       for (int i = lo + (b >> 3) * (WPB) + wave; i < hi; i += step) {
         const uint64_t lm = MASK ? a.lane_masks[i] : ~0ull;
-        acc += process_chunk<FAST, SW, MASK>(a, chunk_of(a, i) * kChunk, lane, lm, i);
+        acc += process_chunk<FAST, SW, MASK>(a, chunk_of(a, i) * kChunk, lane, lm);
       }
     } else if (idx < a.nchunks) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id
@@ -2171,7 +2145,7 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s) {
-  if (!a.nee_post || a.n_nee <= 0) return hipSuccess;
+  if (!a.nee_mac || a.n_nee <= 0) return hipSuccess;
   const dim3 grid((a.n_nee + kBlock - 1) / kBlock);
   typedef void (*Kern)(const MainArgs);
   Kern k;

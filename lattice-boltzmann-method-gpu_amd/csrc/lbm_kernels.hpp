@@ -132,14 +132,10 @@ struct MainArgs {
   const float4* nee_rec;
   const float* nee_in;
   float* nee_out;
-  // NEE posts (nullable; single-domain nee_chunks ranges, LBM_TUNE_NEE_FIX 0): the chunk waves
-  // write each NEE-adjacent cell's post -- kNeePostF4 float4: (rho, ux, uy, uz), then its 19
-  // post-collision populations (and a pad) -- at list index nee_wbase[w] + the cell's rank among
-  // the NEE-adjacent cells of entry wave w (a chunk-list entry, or 64 group-list entries; lanes
-  // in order, a lane's cells in order); k_nee_fix (launch_nee_fix, after the step launch) reads
-  // post i with list entry i and stores the NEE values
-  float4* nee_post;
-  const int* nee_wbase;
+  float4* nee_mac;          // nullable (single-domain nee_chunks ranges, LBM_TUNE_NEE_FIX): the chunk
+                            // waves store each NEE-adjacent cell's (rho, ux, uy, uz) here, indexed by
+                            // cell; k_nee_fix (launch_nee_fix, after the step launch) reads them with
+                            // the cells' own post-collision slots and stores the NEE values
   int swap;             // 1: storage rows run along physical y (Layout::swap)
   // Compact rows (nullable; sparse single-domain lattices, group lists only): every per-cell
   // array above and the population buffers are indexed by compact cell ids -- storage row
@@ -212,13 +208,12 @@ hipError_t launch_nee_records(const int* cells, const int* pos, const uint32_t* 
 // (to_buffer = 1), or back from those slots into vals (0)
 hipError_t launch_nee_materialize(float* f, const float4* rec, float* vals, int n, int pitch, int64_t plane, int swap,
                                   int to_buffer, hipStream_t s);
-// after launch_step of a range with nee_post: one thread per NEE-adjacent cell (cells, cell_nl,
+// after launch_step of a range with nee_mac: one thread per NEE-adjacent cell (cells, cell_nl,
 // nee_bc, n_nee) stores its NEE neighbours' slots of dst
 hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s);
 // NEE directions of a cell whose boundary data is loaded ahead (one flat face: 5); a cell
 // with more (edges and corners of several faces) loads the rest where they are used
 constexpr int kNeeSlots = 5;
-constexpr int kNeePostF4 = 6;  // an NEE post: (rho, u) + 19 populations + pad
 // nee_bc[i * kNeeSlots + j] = (rho, ux, uy, uz) at c_i - e_q, q = the j-th set bit of nl[i]
 // 1 into *differs when some NEE cell's record (rho, ux, uy, uz) differs bitwise from cell ref's
 hipError_t launch_bc_uniform(const uint8_t* type, const float* rho, const float* ux, const float* uy,
