@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Build liblbm.so lab variants for interleaved A/B (tools/ab_lattices.py) into tools/ab/<name>/.
 
-    python3 tools/lab_build.py <name> <patch>[,<patch>...]
+    python3 tools/lab_build.py <name> <patch>[,<patch>...]     # LAB_REV=<git rev>: that revision's csrc/
 
 A patch is a named list of literal (file, old, new) edits applied to a copy of csrc/ (the
 product sources stay untouched); the copy is built with the product's flags.  Lab variants
@@ -112,7 +112,13 @@ def main():
     tmp = tempfile.mkdtemp(prefix="lab_")
     try:
         src = os.path.join(tmp, "pkg", "csrc")  # csrc/../../include/lbm.h as in the tree
-        shutil.copytree(os.path.join(PKG, "csrc"), src)
+        rev = os.environ.get("LAB_REV")  # the sources of a git revision instead of the tree's
+        if rev:
+            os.makedirs(src)
+            arc = subprocess.check_output(["git", "-C", REPO, "archive", rev, "lattice-boltzmann-method-gpu_amd/csrc"])
+            subprocess.run(["tar", "-x", "--strip-components=2", "-C", src], input=arc, check=True)
+        else:
+            shutil.copytree(os.path.join(PKG, "csrc"), src)
         os.symlink(os.path.join(REPO, "include"), os.path.join(tmp, "include"))
         for spec in specs:
             for fname, old, new in PATCHES[spec]:
