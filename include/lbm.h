@@ -209,9 +209,11 @@ typedef enum {
                                    and the next step's wave puts them into its pulls (chunk lists
                                    of the dense box with at most 8 such cells per chunk; otherwise
                                    as 0) */
-  LBM_TUNE_XCD_RUN = 13,        /* order of the step kernel's chunk workgroups over the 8 XCDs: 0 each
-                                   XCD takes one contiguous eighth of the chunks; L = 1..16 runs of
-                                   2^(L-1) workgroups, XCD x taking runs x, x + 8, x + 16, ... */
+  LBM_TUNE_XCD_RUN = 13,        /* order of the step kernel's chunk workgroups over the 8 XCDs: 0
+                                   (default) round robin (as L = 1) for 4-cell chunk lists whose rows
+                                   run along y (the pipe), one contiguous eighth of the chunks per
+                                   XCD elsewhere; L = 1..16 runs of 2^(L-1) workgroups, XCD x taking
+                                   runs x, x + 8, x + 16, ...; 17 one eighth per XCD everywhere */
   LBM_TUNE_COUNT = 14
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);

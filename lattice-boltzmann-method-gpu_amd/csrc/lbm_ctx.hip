@@ -411,7 +411,11 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
-  a.xcd_run = c->xcd_run;
+  // LBM_TUNE_XCD_RUN 0 (auto): round robin (runs of one block) for the 4-cell chunk lists whose
+  // rows run along y -- the pipe, C3: 184 -> 176 us per step in rocprof, where LDC 256^3 and
+  // 512^3 run 9% / 4% slower that way (profiles/r05p_c3_posts_xcd_rocprof.log,
+  // r05_xcd_run_ab.log) -- one contiguous eighth per XCD elsewhere; 17: eighths everywhere
+  a.xcd_run = c->xcd_run == 17 ? 0 : c->xcd_run > 0 ? c->xcd_run : (c->L.swap && !r.quarter && !r.groups) ? 1 : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
   a.groups = r.groups;
   a.ngroups = r.ngroups;
@@ -1210,7 +1214,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 2, 16};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 2, 17};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";

@@ -207,6 +207,31 @@ def test_grid_stride_bitwise(gpu, knob, case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lattice", ["pipe_y", "ldc"])
+def test_xcd_run_bitwise(gpu, knob, lattice):
+    """LBM_TUNE_XCD_RUN changes only which XCD takes which chunk workgroup: a pipe with rows along
+    y (round robin by default) and a cavity (one eighth per XCD by default) under both orders and
+    runs of 16 workgroups step bit for bit alike, residual histories included (each partial slot
+    sums the same chunks whatever the order)."""
+    from lbm_amd import cases
+    knob(gpu.TUNE_CELLS_PER_LANE, 4)
+
+    def run(v):
+        with gpu.tuned(gpu.TUNE_XCD_RUN, v):
+            lat = cases.poiseuille(40, 512, 36)[0] if lattice == "pipe_y" else cases.ldc_device(96, 96, 96)
+        hist = lat.step(9)
+        f = lat.f()
+        lat.close()
+        return f, hist
+
+    f0, h0 = run(0)
+    for v in (17, 1, 5):
+        f, h = run(v)
+        assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), f"{lattice} xcd_run={v}"
+        assert np.array_equal(h.view(np.uint32), h0.view(np.uint32)), (v, h, h0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["bif_x4", "coronary", "pipe"])
 def test_groups_bitwise(gpu, knob, case):
     """LBM_TUNE_GROUPS changes only which lane updates which cells: the upsampled bifurcation and
