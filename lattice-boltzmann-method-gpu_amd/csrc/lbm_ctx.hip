@@ -1635,12 +1635,14 @@ int lbm_set_f(lbm_ctx* c, const float* f) {
         for (int x = 0; x < L.nx; ++x) h[aidx(cell_of(L, x, y, z), q)] = row[x];
       }
   if (c->compact) {
-    Stage st;
-    float* f0 = nullptr;
-    RCK(stage_dense(c, st, &f0));
-    HIPCK(c, hipMemcpyAsync(f0, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice, c->s_comp));
-    for (int b = 0; b < 2; ++b) RCK(from_dense(c, f0, b));
-    HIPCK(c, hipStreamSynchronize(c->s_comp));
+    // gathered into the compact layout on the host through cmap (no dense device copy), as
+    // k_pop_gather would: slots of compact cells without a dense cell read 0
+    std::vector<float> hc((size_t)c->pop_floats(), 0.f);
+    for (size_t i = 0; i < c->cmap_h.size(); ++i)
+      if (c->cmap_h[i] >= 0)
+        for (int q = 0; q < kQ; ++q) hc[aidx((int64_t)i, q)] = h[aidx(c->cmap_h[i], q)];
+    for (int b = 0; b < 2; ++b)
+      HIPCK(c, hipMemcpy(c->buf[b], hc.data(), sizeof(float) * hc.size(), hipMemcpyHostToDevice));
   } else {
     for (int b = 0; b < 2; ++b)
       HIPCK(c, hipMemcpy(c->buf[b], h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
