@@ -1827,18 +1827,20 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
     // the reference's order: per step calc_vel_square's terms into reference storage order, then
     // thrust::reduce's CUB tree in fp32 (ldc.cu:660-668)
     const Layout& L = c->L;
-    Stage st;
-    float* dense = nullptr;
-    if (c->compact) RCK(stage_dense(c, st, &dense));
     for (int s = 0; s < nsteps; ++s) {
       const int k = c->steps_done + s;
       RCK(run_range(c, c->whole, c->cur, c->s_comp, nullptr, -1, nullptr, k));
       const float* src = c->buf[c->cur];
-      if (c->compact) {  // the terms from a dense copy (test path: one extra copy per step)
-        RCK(to_dense(c, c->cur, dense));
-        src = dense;
+      const bool own = c->bb_pull() && !c->bb_raw(k);  // wall links read the own slots
+      if (c->compact) {  // over the compact rows, each term into its dense cell's reference slot
+        HIPCK(c, launch_vel_terms_compact(src, c->ctype, own ? c->clinks : nullptr, c->cmap, c->crow, c->rowrec,
+                                          c->ref_idx, c->terms, c->whole.c_lo, c->whole.c_hi, L.swap, c->s_comp));
+        c->cur ^= 1;
+        HIPCK(c, launch_cub_tree(c->terms, c->n_ref, c->cub_ipt, c->cub_vec, c->cub_grid, c->cub_part, c->conv,
+                                 want_hist ? c->hist + s : nullptr, c->s_comp));
+        continue;
       }
-      const uint32_t* bbl = (c->bb_pull() && !c->bb_raw(k)) ? c->links : nullptr;
+      const uint32_t* bbl = own ? c->links : nullptr;
       if (c->whole.nee_records && k >= 1)  // the step's source with its NEE slots (the records of step k - 1)
         HIPCK(c, launch_nee_materialize(c->buf[c->cur], c->whole.nee_rec,
                                         c->nee_val + (int64_t)((k - 1) & 1) * c->whole.n_rec * 8, c->whole.n_rec,
@@ -1849,7 +1851,6 @@ int step_single(lbm_ctx* c, int nsteps, bool want_hist) {
       HIPCK(c, launch_cub_tree(c->terms, c->n_ref, c->cub_ipt, c->cub_vec, c->cub_grid, c->cub_part, c->conv,
                                want_hist ? c->hist + s : nullptr, c->s_comp));
     }
-    if (c->compact) HIPCK(c, hipStreamSynchronize(c->s_comp));  // before the staging copy is freed
     return LBM_OK;
   }
   if (c->fuse_red && !c->conv_enabled) {

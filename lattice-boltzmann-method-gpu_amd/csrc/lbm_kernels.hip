@@ -1897,6 +1897,30 @@ __global__ void k_vel_terms(const float* __restrict__ src, const uint8_t* __rest
   }
 }
 
+// the same over compact rows (cell i pulls through its row record as k_moments_compact does),
+// each term into the reference slot of its dense cell cmap[i]
+template <bool SW>
+__global__ void k_vel_terms_compact(const float* __restrict__ src, const uint8_t* __restrict__ type,
+                                    const uint32_t* bb_links, const int* __restrict__ cmap,
+                                    const int* __restrict__ row_of, const int4* __restrict__ rowrec,
+                                    const int* __restrict__ ref_idx, float* __restrict__ terms, int64_t lo, int64_t hi) {
+  for (int64_t c = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < hi; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t t = type[c];
+    const int d = cmap[c];
+    if ((t & kClassMask) != kFluid || d < 0) continue;
+    float f[kQ];
+    pull1_bb<SW>(f, src, Rows::load(rowrec, c, row_of[c >> 2]), compact_id(c),
+                 (bb_links && (t & kWallAdj)) ? bb_links[c] : 0u, AllQ{});
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) r = r + f[q];
+    const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / r;
+    const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / r;
+    const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / r;
+    terms[ref_idx[d]] = sqrtf(ux * ux + uy * uy + uz * uz);
+  }
+}
+
 // CUB's block reduction (BLOCK_REDUCE_WARP_REDUCTIONS) with 32-lane logical warps on the
 // 64-lane wavefront: a shuffle-down tree per warp (offsets 1 .. 16; a lane adds its partner's
 // value only when the partner holds data), then thread 0 adds the warp sums in warp order.
@@ -2427,6 +2451,20 @@ hipError_t launch_vel_terms(const float* src, const uint8_t* type, const uint32_
   else
     hipLaunchKernelGGL(k_vel_terms<false>, g, dim3(256), 0, s, src, type, bb_links, ref_idx, terms, lo, hi, pitch,
                        plane);
+  return hipGetLastError();
+}
+
+hipError_t launch_vel_terms_compact(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* cmap,
+                                    const int* row_of, const int4* rowrec, const int* ref_idx, float* terms, int64_t lo,
+                                    int64_t hi, int swap, hipStream_t s) {
+  if (hi <= lo) return hipSuccess;
+  const dim3 g(grid_for(hi - lo, 256));
+  if (swap)
+    hipLaunchKernelGGL(k_vel_terms_compact<true>, g, dim3(256), 0, s, src, type, bb_links, cmap, row_of, rowrec, ref_idx,
+                       terms, lo, hi);
+  else
+    hipLaunchKernelGGL(k_vel_terms_compact<false>, g, dim3(256), 0, s, src, type, bb_links, cmap, row_of, rowrec,
+                       ref_idx, terms, lo, hi);
   return hipGetLastError();
 }
 

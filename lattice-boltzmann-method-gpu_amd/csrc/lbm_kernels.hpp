@@ -243,6 +243,11 @@ hipError_t launch_finish_global(ConvState* conv, float* hist_slot, hipStream_t s
 // partials, then the residual logic on S = 0.f + the tree's sum
 hipError_t launch_vel_terms(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* ref_idx,
                             float* terms, int64_t lo, int64_t hi, int pitch, int64_t plane, int swap, hipStream_t s);
+// the same over compact rows (type, bb_links, row_of, rowrec by compact cell; cmap: compact ->
+// dense cell; ref_idx by dense cell)
+hipError_t launch_vel_terms_compact(const float* src, const uint8_t* type, const uint32_t* bb_links, const int* cmap,
+                                    const int* row_of, const int4* rowrec, const int* ref_idx, float* terms, int64_t lo,
+                                    int64_t hi, int swap, hipStream_t s);
 int cub_grid(int64_t n, int ipt, int grid_cap);
 hipError_t launch_cub_tree(const float* terms, int64_t n, int ipt, int vec, int grid_cap, float* partials,
                            ConvState* conv, float* hist_slot, hipStream_t s);

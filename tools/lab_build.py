@@ -101,6 +101,13 @@ PATCHES = {
     # the one-cell paths' stores non-temporal
     "t1_ntstores": [("lbm_kernels.hip", "  ((dst[aidx(c, Qs)] = f[Qs]), ...);\n  if (m) {",
                      "  (__builtin_nontemporal_store(f[Qs], dst + aidx(c, Qs)), ...);\n  if (m) {")],
+    # k_nee_fix in one-wave workgroups (spread over all CUs)
+    "fix64": [("lbm_kernels.hip", "  const int i = blockIdx.x * kBlock + (int)threadIdx.x;",
+               "  const int i = blockIdx.x * 64 + (int)threadIdx.x;"),
+              ("lbm_kernels.hip", "  const dim3 grid((a.n_nee + kBlock - 1) / kBlock);\n  typedef void (*Kern)(const MainArgs);\n  Kern k;\n  if (a.rowrec) k = a.swap ? k_nee_fix",
+               "  const dim3 grid((a.n_nee + 63) / 64);\n  typedef void (*Kern)(const MainArgs);\n  Kern k;\n  if (a.rowrec) k = a.swap ? k_nee_fix"),
+              ("lbm_kernels.hip", "  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, s, a);\n  return hipGetLastError();\n}\n\nhipError_t launch_reduce(",
+               "  hipLaunchKernelGGL(k, grid, dim3(64), 0, s, a);\n  return hipGetLastError();\n}\n\nhipError_t launch_reduce(")],
     # every 4-cell whole store plain
     "t4_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
                    "    for (int q = 0; q < kQ; ++q) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];")],

@@ -44,6 +44,9 @@ def main():
               if "k_step" in r["Name"]]
         calls = sum(int(r["Calls"]) for r in kt)
         avg_ns = sum(float(r["TotalDurationNs"]) for r in kt) / max(1, calls)
+        fx = [r for r in csv.DictReader(open(glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))[0]))
+              if "k_nee_fix" in r["Name"]]
+        fix_ns = sum(float(r["TotalDurationNs"]) for r in fx) / max(1, sum(int(r["Calls"]) for r in fx))
         fe = counters(os.path.join(d, "fetch", "*counter_collection.csv")).get("FETCH_SIZE", 0.0)
         wr = counters(os.path.join(d, "write", "*counter_collection.csv")).get("WRITE_SIZE", 0.0)
         sq = counters(os.path.join(d, "sq", "*counter_collection.csv"))
@@ -56,7 +59,12 @@ def main():
             "algo_bytes_per_launch": int(algo), "traffic_over_algo": round((rd_b + wr_b) / algo, 3) if algo else None,
             "achieved_algo_gbs": round(algo / avg_ns, 1) if avg_ns else None,
             "frac_of_8tbs": round(algo / avg_ns / 8000.0, 4) if avg_ns else None,
+            "k_nee_fix_avg_us": round(fix_ns / 1e3, 3) if fx else None,
             "sq_per_launch": {k: round(v, 1) for k, v in sorted(sq.items())},
+            # 1024 SIMDs; SQ_WAIT_ANY / SQ_WAVE_CYCLES: the share of wave-cycles spent waiting
+            "waves_per_simd": round(sq["SQ_WAVES"] / 1024.0, 2) if sq.get("SQ_WAVES") else None,
+            "wait_share": round(sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"], 3) if sq.get("SQ_WAVE_CYCLES") else None,
+            "reads_over_algo": round(rd_b / (76.0 * ab["n_fluid"]), 3) if ab["n_fluid"] else None,
             "tag": tag, "kernel_src": abl.get("kernel_src"),
         }
         print(case, json.dumps(out[case]))
