@@ -1277,10 +1277,12 @@ __device__ __forceinline__ void own_slots(float* f, const float* __restrict__ ds
                                           std::integer_sequence<int, Qs...>) {
   ((f[Qs] = ((nl >> Qs) & 1u) ? dst[fidx(c, Qs)] : 0.0f), ...);
 }
+// One-wave workgroups: the list's few hundred waves spread over all CUs (C4 x4 133.3 -> 132.4,
+// C3 185.9 -> 185.4 us per step against four-wave ones, profiles/r05_fix64_ab.log)
 template <bool SW, bool COMPACT>
-__global__ __launch_bounds__(kBlock) void k_nee_fix(const MainArgs a) {
+__global__ __launch_bounds__(64) void k_nee_fix(const MainArgs a) {
   if (a.stopped != nullptr && *a.stopped) return;  // uniform: converged, the step was a no-op
-  const int i = blockIdx.x * kBlock + (int)threadIdx.x;
+  const int i = blockIdx.x * 64 + (int)threadIdx.x;
   if (i >= a.n_nee) return;
   const int64_t c = a.cells[i];
   const uint32_t nl = a.cell_nl[i];
@@ -2170,12 +2172,12 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
 
 hipError_t launch_nee_fix(const MainArgs& a, hipStream_t s) {
   if (!a.nee_mac || a.n_nee <= 0) return hipSuccess;
-  const dim3 grid((a.n_nee + kBlock - 1) / kBlock);
+  const dim3 grid((a.n_nee + 63) / 64);
   typedef void (*Kern)(const MainArgs);
   Kern k;
   if (a.rowrec) k = a.swap ? k_nee_fix<true, true> : k_nee_fix<false, true>;
   else k = a.swap ? k_nee_fix<true, false> : k_nee_fix<false, false>;
-  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k, grid, dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
