@@ -108,6 +108,9 @@ PATCHES = {
                "  const dim3 grid((a.n_nee + 63) / 64);\n  typedef void (*Kern)(const MainArgs);\n  Kern k;\n  if (a.rowrec) k = a.swap ? k_nee_fix"),
               ("lbm_kernels.hip", "  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, s, a);\n  return hipGetLastError();\n}\n\nhipError_t launch_reduce(",
                "  hipLaunchKernelGGL(k, grid, dim3(64), 0, s, a);\n  return hipGetLastError();\n}\n\nhipError_t launch_reduce(")],
+    # the compact one-cell kernel in four-wave / one-wave workgroups
+    "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
+    "c1_wg64": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 64;")],
     # every 4-cell whole store plain
     "t4_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
                    "    for (int q = 0; q < kQ; ++q) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];")],
