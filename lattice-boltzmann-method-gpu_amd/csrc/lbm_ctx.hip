@@ -1050,8 +1050,39 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
     std::vector<int> order(ncand);
     for (int i = 0; i < ncand; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return c->cand_gbs[a] > c->cand_gbs[b]; });
-    c->chosen[0] = std::min(order[0], order[1]);  // keep allocation order between the two
-    c->chosen[1] = std::max(order[0], order[1]);
+    int ka = order[0], kb = order[1];
+    if (g_tune[LBM_TUNE_BUFFER_ALLOC] == 2) {
+      // pair probe: among the four fastest writers, the pair whose copies both ways -- k_step's
+      // 16-KB wave tiles, read one buffer, write the other -- take the least time together
+      const int K = std::min(ncand, 4);
+      const int64_t t4 = (int64_t)(bytes / 65536) * 4096;
+      float t[4][4] = {};
+      hipEvent_t a0 = nullptr, a1 = nullptr;
+      e = hipEventCreate(&a0);
+      if (e == hipSuccess) e = hipEventCreate(&a1);
+      for (int i = 0; i < K && e == hipSuccess; ++i)
+        for (int j = 0; j < K && e == hipSuccess; ++j) {
+          if (i == j) continue;
+          e = launch_probe_copy(p[order[i]], p[order[j]], t4, 0, 6, c->s_comp);  // warm-up
+          if (e == hipSuccess) e = hipEventRecord(a0, c->s_comp);
+          for (int r = 0; r < 2 && e == hipSuccess; ++r) e = launch_probe_copy(p[order[i]], p[order[j]], t4, 0, 6, c->s_comp);
+          if (e == hipSuccess) e = hipEventRecord(a1, c->s_comp);
+          if (e == hipSuccess) e = hipEventSynchronize(a1);
+          if (e == hipSuccess) e = hipEventElapsedTime(&t[i][j], a0, a1);
+        }
+      if (a0) (void)hipEventDestroy(a0);
+      if (a1) (void)hipEventDestroy(a1);
+      float best = 0.f;
+      for (int i = 0; i < K; ++i)
+        for (int j = i + 1; j < K; ++j)
+          if (best == 0.f || t[i][j] + t[j][i] < best) {
+            best = t[i][j] + t[j][i];
+            ka = order[i];
+            kb = order[j];
+          }
+    }
+    c->chosen[0] = std::min(ka, kb);  // keep allocation order between the two
+    c->chosen[1] = std::max(ka, kb);
   }
   for (int i = 0; i < (int)p.size(); ++i) {
     if (e == hipSuccess && (i == c->chosen[0] || i == c->chosen[1]))
@@ -1214,7 +1245,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 1, 86400, 8, 0, 2, 64, 2, 1, 2, 17};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 2, 17};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";

@@ -109,7 +109,7 @@ def test_tune_knobs_validated(lbm):
                         (lbm.TUNE_CELLS_PER_LANE, 3), (lbm.TUNE_EXACT_DIV, -1), (lbm.TUNE_SYNC_TIMEOUT_S, 86401),
                         (lbm.TUNE_GRID_STRIDE, 9), (lbm.TUNE_INJECT_RCCL_FAULT, 1), (lbm.TUNE_GROUPS, 3),
                         (lbm.TUNE_GROUP_SEGMENT, 65), (lbm.TUNE_COMPACT, 3), (lbm.TUNE_BOX, 2),
-                        (lbm.TUNE_NEE_FIX, 3), (lbm.TUNE_XCD_RUN, 18)):
+                        (lbm.TUNE_NEE_FIX, 3), (lbm.TUNE_XCD_RUN, 18), (lbm.TUNE_BUFFER_ALLOC, 3)):
         with pytest.raises(lbm.LbmError, match="unknown knob or value"):
             lbm.tune(knob, value)
     for knob, dflt in defaults.items():  # a rejected call leaves every knob as it was
