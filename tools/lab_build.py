@@ -111,6 +111,9 @@ PATCHES = {
     # the compact one-cell kernel in four-wave / one-wave workgroups
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
     "c1_wg64": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 64;")],
+    # placement over up to 160 GiB of candidates (15 at 512^3 instead of 6)
+    "budget160": [("lbm_ctx.hip", "constexpr size_t kPlacementBudget = (size_t)64 << 30;",
+                   "constexpr size_t kPlacementBudget = (size_t)160 << 30;")],
     # every 4-cell whole store plain
     "t4_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
                    "    for (int q = 0; q < kQ; ++q) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];")],
