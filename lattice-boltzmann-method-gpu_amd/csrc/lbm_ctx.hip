@@ -1004,7 +1004,7 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
   constexpr int kMaxCand = 16;
   int ncand = 2;
   const bool probe = bytes > kPlacementMinBytes;
-  if (!g_tune[LBM_TUNE_BUFFER_ALLOC] && probe) {
+  if (g_tune[LBM_TUNE_BUFFER_ALLOC] != 1 && probe) {
     size_t fr = 0, tot = 0;
     hipError_t e = hipMemGetInfo(&fr, &tot);
     if (e != hipSuccess) return e;

@@ -30,6 +30,7 @@ def child(which):
 
     def run(lat, steps):
         shape = lat.launch_shape()
+        place = lat.placement()
         nf = lat.counts()["n_fluid"]
         lat.step(20, history=False)
         lat.sync()
@@ -43,7 +44,7 @@ def child(which):
         lat.close()
         return {"us_step": round(dt / steps * 1e6, 2),
                 "k_step_us": round(st["step_kernel_ms"] / max(1, st["step_kernel_launches"]) * 1e3, 2),
-                "n_fluid": nf, "launch_shape": shape}
+                "n_fluid": nf, "launch_shape": shape, "placement": place}
 
     out = {}
     for w in which.split(","):
