@@ -187,7 +187,7 @@ typedef enum {
                                    3/4 busy, 1 never, 2 on every sparse list.  With CELLS_PER_LANE 0
                                    a list of at most 8192 x 64 groups runs one cell per lane (16
                                    groups per wave), a longer one four (64 per wave) */
-  LBM_TUNE_GROUP_SEGMENT = 9,   /* group lists: 1..64 groups per segment (default 8: one 128-B line);
+  LBM_TUNE_GROUP_SEGMENT = 9,   /* group lists: 1..64 groups per segment (default 16: two 128-B lines);
                                    a segment with an active group enters the list whole, its idle
                                    groups load nothing */
   LBM_TUNE_COMPACT = 10,        /* storage of single-domain lattices whose step takes group lists

@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 8, 0, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -714,11 +714,12 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     const bool sparse = r.quarter ? r.lane_fill < kGroupFill1 : r.lane_masks && r.lane_fill < 0.75;
     const bool want = cv || gm == 2 || (gm == 0 && (sparse || group1));
     if (r.nchunks && (r.chunk0 < 0 || cv) && want) {
-      // segments of seg groups (LBM_TUNE_GROUP_SEGMENT, default 8 = one 128-B line of a chunk
+      // segments of seg groups (LBM_TUNE_GROUP_SEGMENT, default 16 = two 128-B lines of a chunk
       // slice): a segment with an active group enters the list whole, its idle groups marked
       // (bit 0) so their lanes load nothing.  Whole lines per wave load beat full lanes on the
       // coronary tree (59 vs 73 us per step with single groups), and cost the upsampled
-      // bifurcation, whose runs are long anyway, 3% (profiles/r03_groups_ab.log)
+      // bifurcation, whose runs are long anyway, 3% (profiles/r03_groups_ab.log); with plain
+      // loads (round 5) 16 groups beat 8 on C4 x4, 133.1 -> 131.8 us (r05_c4x4_segment_ab.log)
       const int seg = std::max(1, g_tune[LBM_TUNE_GROUP_SEGMENT]);
       std::vector<int> gl;
       int64_t cells_in = 0;

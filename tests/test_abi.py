@@ -98,7 +98,7 @@ def test_tune_knobs_validated(lbm):
     defaults = {lbm.TUNE_ROW_AXIS: 0, lbm.TUNE_CELLS_PER_LANE: 0, lbm.TUNE_EXACT_DIV: 0,
                 lbm.TUNE_FUSED_RESIDUAL: 1, lbm.TUNE_BUFFER_ALLOC: 0, lbm.TUNE_SYNC_TIMEOUT_S: 0,
                 lbm.TUNE_GRID_STRIDE: 0, lbm.TUNE_INJECT_RCCL_FAULT: 0, lbm.TUNE_GROUPS: 0,
-                lbm.TUNE_GROUP_SEGMENT: 8, lbm.TUNE_COMPACT: 0, lbm.TUNE_BOX: 0, lbm.TUNE_NEE_FIX: 0,
+                lbm.TUNE_GROUP_SEGMENT: 16, lbm.TUNE_COMPACT: 0, lbm.TUNE_BOX: 0, lbm.TUNE_NEE_FIX: 0,
                 lbm.TUNE_XCD_RUN: 0}
     for knob, dflt in defaults.items():
         assert lbm.tune(knob, dflt) == dflt
