@@ -167,10 +167,10 @@ typedef enum {
   LBM_TUNE_CELLS_PER_LANE = 1,  /* step kernel: 0 by size, 1 one cell per lane, 4 four */
   LBM_TUNE_EXACT_DIV = 2,       /* 1: the compiler's division by tau everywhere */
   LBM_TUNE_FUSED_RESIDUAL = 3,  /* 1 (default): the residual rides in the next step's launch */
-  LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 (default) the two fastest-writing of up
-                                   to sixteen allocations (lbm_buffer_placement), 1 the first two,
-                                   2 of the four fastest-writing, the pair whose tile copies both
-                                   ways take the least time together */
+  LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 (default) of the four fastest-writing of
+                                   up to sixteen allocations (lbm_buffer_placement), the pair whose
+                                   tile copies both ways take the least time together; 1 the first
+                                   two allocations; 2 the two fastest-writing (round 4) */
   LBM_TUNE_SYNC_TIMEOUT_S = 5,  /* RCCL contexts: a wait (lbm_sync, synchronising lbm_step, read-
                                    outs) longer than this many seconds aborts the communicator
                                    and fails with LBM_ERR_RCCL; 0 (default): no limit.  A peer's

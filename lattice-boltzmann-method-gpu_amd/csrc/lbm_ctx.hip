@@ -988,19 +988,20 @@ int prime_walls(lbm_ctx* c) {
 // gpurun_out/r02g-i).  A copy runs at its destination's rate, and k_step writes one buffer per
 // step, so a slow buffer costs every other step ~8% (the 3.4 / 3.7 ms alternation at 512^3).
 // When the device has room (hipMemGetInfo, after `others` bytes for the remaining arrays), up to
-// four extra candidates are allocated, each zeroed and timed over one full-buffer sweep of
-// non-temporal 16-B stores, and the two fastest kept; the rest are freed before any other array
-// is allocated.  Every buffer larger than the 256-MB MALL is probed (round 4 probed only
+// fourteen extra candidates are allocated, each zeroed and timed over one full-buffer sweep of
+// non-temporal 16-B stores; of the four fastest, the pair whose tile copies both ways are
+// quickest is kept, and the rest are freed before any other array is allocated.  Every buffer larger than the 256-MB MALL is probed (round 4 probed only
 // buffers >= 1 GiB, so the 647-MB buffers of the C3 pipe took whatever came first); smaller
 // ones (MALL resident, latency-bound) and LBM_TUNE_BUFFER_ALLOC = 1 take the first two
 // allocations (the latter still timed, for A/B).
-// The candidates take at most kPlacementBudget bytes together (six at 512^3) and number at most
+// The candidates take at most kPlacementBudget bytes together (15 at 512^3: 3297.7 against
+// 3336.6 us per step with the round-4 budget's six, profiles/r05s_placement.log) and number at most
 // kMaxCand: at LDC 256^3 (1.28-GB buffers) one or two of six candidates wrote at ~6.1 TB/s and
 // the rest at 4.9-5.6, so the step that writes the slower kept buffer ran 433 instead of 422 us,
 // and the first two allocations (no probe) 457 us (gpurun_out/r05a, tools/ab_alloc.py); more
 // candidates make a pair of fast ones likelier.
 constexpr size_t kPlacementMinBytes = (size_t)256 << 20;
-constexpr size_t kPlacementBudget = (size_t)64 << 30;
+constexpr size_t kPlacementBudget = (size_t)160 << 30;
 hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
   constexpr int kMaxCand = 16;
   int ncand = 2;
@@ -1052,9 +1053,11 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
     for (int i = 0; i < ncand; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return c->cand_gbs[a] > c->cand_gbs[b]; });
     int ka = order[0], kb = order[1];
-    if (g_tune[LBM_TUNE_BUFFER_ALLOC] == 2) {
+    if (g_tune[LBM_TUNE_BUFFER_ALLOC] == 0) {
       // pair probe: among the four fastest writers, the pair whose copies both ways -- k_step's
       // 16-KB wave tiles, read one buffer, write the other -- take the least time together
+      // (LDC 256^3 in one process, four fresh lattices each: 422.9 against 427.7 us per step
+      // for the two fastest writers, profiles/r05s_placement.log)
       const int K = std::min(ncand, 4);
       const int64_t t4 = (int64_t)(bytes / 65536) * 4096;
       float t[4][4] = {};
