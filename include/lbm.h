@@ -318,8 +318,9 @@ int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
 /* Placement of the two population buffers (not a reference interface).  HBM write bandwidth
  * differs between allocations (~5.5 vs ~6.4 TB/s for 10-GB buffers on MI355X, stable per
  * allocation); when a buffer is larger than 256 MB (the MALL) and the device has room,
- * lbm_create allocates up to sixteen candidates (at most 64 GiB together: six at 512^3), times
- * one full-buffer write sweep of each and keeps the two fastest.  gbs[0..cap) receives the
+ * lbm_create allocates up to sixteen candidates (at most 160 GiB together: 15 at 512^3), times
+ * one full-buffer write sweep of each and, of the four fastest, keeps the pair whose tile copies
+ * both ways take the least time together (LBM_TUNE_BUFFER_ALLOC).  gbs[0..cap) receives the
  * candidates' rates (GB/s) in allocation order, *n their count (0: buffers of at most 256 MB,
  * or compact rows, not probed), chosen[2] the indices kept.  Nullable outputs. */
 int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen);
