@@ -497,8 +497,9 @@ def main():
             "frac_of_stream_probe": round(achieved / probe, 4) if probe else None,
             "stream_probe": "lbm_probe_stream: best of 11 streaming-copy shapes (16-B vectors, grid-stride, "
                             "per-XCD regions or k_step-like 16-KB wave tiles, plain or non-temporal, the tiles also by "
-                            "LDS-DMA; read + write bytes / time) between the two fastest-writing of up to six 8-GiB "
-                            "allocations (the population buffers' placement rule) on this GPU in this run",
+                            "LDS-DMA; read + write bytes / time) between two of up to sixteen 8-GiB allocations, picked by "
+                            "the population buffers' placement rule (write-sweep rank, then the quickest tile-copy "
+                            "pair of the four fastest) on this GPU in this run",
             "stream_probe_shapes_gbs": probe_shapes,
         },
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},

@@ -353,7 +353,8 @@ int lbm_get_storage(lbm_ctx* ctx, int* compact, int64_t* cells, int64_t* bytes);
  * one wave per 16-KB tile with all 16 loads per lane in flight, and that tile by LDS-DMA), `reps` timed
  * launches each (HIP events, after one untimed launch); *gbs = the best (read + write bytes) /
  * duration in GB/s.  The two buffers are picked as the population buffers are
- * (lbm_buffer_placement): the two fastest-writing of up to six allocations of `bytes`. */
+ * (lbm_buffer_placement): of up to sixteen allocations of `bytes`, the pair among the four
+ * fastest-writing whose tile copies both ways take the least time together. */
 int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs);
 /* The same, per copy shape: gbs_shape[i] = the best rate of shape i for i < min(cap, n);
  * *n = the number of shapes (grid-stride / per-XCD-region copies, k_step's 16-KB wave tiles by

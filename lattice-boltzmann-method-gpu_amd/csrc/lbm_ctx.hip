@@ -1000,6 +1000,58 @@ int prime_walls(lbm_ctx* c) {
 // the rest at 4.9-5.6, so the step that writes the slower kept buffer ran 433 instead of 422 us,
 // and the first two allocations (no probe) 457 us (gpurun_out/r05a, tools/ab_alloc.py); more
 // candidates make a pair of fast ones likelier.
+// Ranks equal-sized candidate allocations p (zeroed) by one timed write sweep each (gbs: GB/s,
+// allocation order) and picks two: with pair_probe, among the four fastest writers the pair whose
+// copies both ways -- k_step's 16-KB wave tiles, one buffer read, the other written -- take the
+// least time together (LDC 256^3 in one process, four fresh lattices each: 422.9 against 427.7 us
+// per step for the two fastest writers, profiles/r05s_placement.log); else the two fastest.
+hipError_t rank_pair(const std::vector<void*>& p, size_t bytes, hipStream_t st, bool pair_probe,
+                     std::vector<double>& gbs, int& ka, int& kb) {
+  const int n = (int)p.size();
+  const int64_t n4 = (int64_t)(bytes / 16);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  auto timed_ms = [&](auto&& launch, int reps, float& ms) {
+    e = launch();  // warm-up (the memset's shape differs)
+    if (e == hipSuccess) e = hipEventRecord(e0, st);
+    for (int r = 0; r < reps && e == hipSuccess; ++r) e = launch();
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  };
+  gbs.clear();
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    float ms = 0.f;
+    timed_ms([&] { return launch_probe_fill(p[i], n4, st); }, 1, ms);
+    gbs.push_back(ms > 0.f ? (double)bytes / (ms * 1e-3) / 1e9 : 0.0);
+  }
+  std::vector<int> order(n);
+  for (int i = 0; i < n; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return gbs[a] > gbs[b]; });
+  ka = order[0];
+  kb = order[1];
+  if (pair_probe && n > 2 && e == hipSuccess) {
+    const int K = std::min(n, 4);
+    const int64_t t4 = (int64_t)(bytes / 65536) * 4096;
+    float t[4][4] = {};
+    for (int i = 0; i < K && e == hipSuccess; ++i)
+      for (int j = 0; j < K && e == hipSuccess; ++j)
+        if (i != j) timed_ms([&] { return launch_probe_copy(p[order[i]], p[order[j]], t4, 0, 6, st); }, 2, t[i][j]);
+    float best = 0.f;
+    for (int i = 0; i < K; ++i)
+      for (int j = i + 1; j < K; ++j)
+        if (best == 0.f || t[i][j] + t[j][i] < best) {
+          best = t[i][j] + t[j][i];
+          ka = order[i];
+          kb = order[j];
+        }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  return e;
+}
+
 constexpr size_t kPlacementMinBytes = (size_t)256 << 20;
 constexpr size_t kPlacementBudget = (size_t)160 << 30;
 hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
@@ -1014,11 +1066,10 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
     const int cap = (int)std::max<size_t>(2, std::min<size_t>(kMaxCand, kPlacementBudget / bytes));
     if (fr > need) ncand = (int)std::min<size_t>(cap, 2 + (fr - need) / bytes);
   }
-  std::vector<float*> p;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<void*> p;
   hipError_t e = hipSuccess;
   for (int i = 0; i < ncand && e == hipSuccess; ++i) {
-    float* q = nullptr;
+    void* q = nullptr;
     e = hipMalloc(&q, bytes);
     if (e != hipSuccess) {
       if (i >= 2) {  // out of room after all: probe what we have
@@ -1032,65 +1083,14 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
     e = hipMemsetAsync(q, 0, bytes, c->s_comp);
   }
   if (e == hipSuccess && probe) {
-    const int64_t n4 = (int64_t)(bytes / 16);
-    e = hipEventCreate(&e0);
-    if (e == hipSuccess) e = hipEventCreate(&e1);
-    for (int i = 0; i < ncand && e == hipSuccess; ++i) {
-      e = launch_probe_fill(p[i], n4, c->s_comp);  // warm-up sweep (the memset's shape differs)
-      if (e == hipSuccess) e = hipEventRecord(e0, c->s_comp);
-      if (e == hipSuccess) e = launch_probe_fill(p[i], n4, c->s_comp);
-      if (e == hipSuccess) e = hipEventRecord(e1, c->s_comp);
-      if (e == hipSuccess) e = hipEventSynchronize(e1);
-      float ms = 0.f;
-      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-      c->cand_gbs.push_back(ms > 0.f ? (double)bytes / (ms * 1e-3) / 1e9 : 0.0);
-    }
-  }
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  if (e == hipSuccess && ncand > 2) {
-    std::vector<int> order(ncand);
-    for (int i = 0; i < ncand; ++i) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return c->cand_gbs[a] > c->cand_gbs[b]; });
-    int ka = order[0], kb = order[1];
-    if (g_tune[LBM_TUNE_BUFFER_ALLOC] == 0) {
-      // pair probe: among the four fastest writers, the pair whose copies both ways -- k_step's
-      // 16-KB wave tiles, read one buffer, write the other -- take the least time together
-      // (LDC 256^3 in one process, four fresh lattices each: 422.9 against 427.7 us per step
-      // for the two fastest writers, profiles/r05s_placement.log)
-      const int K = std::min(ncand, 4);
-      const int64_t t4 = (int64_t)(bytes / 65536) * 4096;
-      float t[4][4] = {};
-      hipEvent_t a0 = nullptr, a1 = nullptr;
-      e = hipEventCreate(&a0);
-      if (e == hipSuccess) e = hipEventCreate(&a1);
-      for (int i = 0; i < K && e == hipSuccess; ++i)
-        for (int j = 0; j < K && e == hipSuccess; ++j) {
-          if (i == j) continue;
-          e = launch_probe_copy(p[order[i]], p[order[j]], t4, 0, 6, c->s_comp);  // warm-up
-          if (e == hipSuccess) e = hipEventRecord(a0, c->s_comp);
-          for (int r = 0; r < 2 && e == hipSuccess; ++r) e = launch_probe_copy(p[order[i]], p[order[j]], t4, 0, 6, c->s_comp);
-          if (e == hipSuccess) e = hipEventRecord(a1, c->s_comp);
-          if (e == hipSuccess) e = hipEventSynchronize(a1);
-          if (e == hipSuccess) e = hipEventElapsedTime(&t[i][j], a0, a1);
-        }
-      if (a0) (void)hipEventDestroy(a0);
-      if (a1) (void)hipEventDestroy(a1);
-      float best = 0.f;
-      for (int i = 0; i < K; ++i)
-        for (int j = i + 1; j < K; ++j)
-          if (best == 0.f || t[i][j] + t[j][i] < best) {
-            best = t[i][j] + t[j][i];
-            ka = order[i];
-            kb = order[j];
-          }
-    }
+    int ka = 0, kb = 1;
+    e = rank_pair(p, bytes, c->s_comp, g_tune[LBM_TUNE_BUFFER_ALLOC] == 0, c->cand_gbs, ka, kb);
     c->chosen[0] = std::min(ka, kb);  // keep allocation order between the two
     c->chosen[1] = std::max(ka, kb);
   }
   for (int i = 0; i < (int)p.size(); ++i) {
     if (e == hipSuccess && (i == c->chosen[0] || i == c->chosen[1]))
-      c->alloc[i == c->chosen[0] ? 0 : 1] = p[i];
+      c->alloc[i == c->chosen[0] ? 0 : 1] = static_cast<float*>(p[i]);
     else
       (void)hipFree(p[i]);
   }
@@ -2443,42 +2443,34 @@ int lbm_probe_stream_shapes(int device, int64_t bytes, int reps, double* gbs_sha
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
-  // the same placement rule as the population buffers (buffer_placement): an allocation
-  // sweep-writes at ~6.4 or ~5.5 TB/s for its lifetime, so up to six candidates are timed over
-  // one write sweep each and the copies run between the two fastest
+  // the same placement rule as the population buffers (buffer_placement, rank_pair): up to
+  // sixteen candidates within the same budget, ranked by a write sweep each, and of the four
+  // fastest the pair whose tile copies both ways take the least time together
   {
     std::vector<void*> cand;
     std::vector<double> rate;
     size_t fr = 0, tot = 0;
     if (e == hipSuccess) e = hipMemGetInfo(&fr, &tot);
     const size_t sz = (size_t)n4 * 16;
-    const int ncand = (int)std::max<size_t>(2, std::min<size_t>(6, fr > sz ? (fr - sz) / sz : 0));
+    const int ncand = (int)std::max<size_t>(
+        2, std::min<size_t>(std::min<size_t>(16, kPlacementBudget / sz), fr > sz ? (fr - sz) / sz : 0));
     for (int i = 0; i < ncand && e == hipSuccess; ++i) {
       void* q = nullptr;
       e = hipMalloc(&q, sz);
       if (e != hipSuccess) break;
       cand.push_back(q);
       e = hipMemsetAsync(q, 0x3c, sz, st);
-      if (e == hipSuccess) e = launch_probe_fill(q, n4, st);  // warm-up sweep
-      if (e == hipSuccess) e = hipEventRecord(e0, st);
-      if (e == hipSuccess) e = launch_probe_fill(q, n4, st);
-      if (e == hipSuccess) e = hipEventRecord(e1, st);
-      if (e == hipSuccess) e = hipEventSynchronize(e1);
-      float ms = 0.f;
-      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-      rate.push_back(ms > 0.f ? (double)sz / ms : 0.0);
     }
     if (e == hipErrorOutOfMemory && cand.size() >= 2) {
       (void)hipGetLastError();
       e = hipSuccess;
     }
-    std::vector<int> order(cand.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
-    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return rate[x] > rate[y]; });
-    for (size_t k = 0; k < order.size(); ++k) {
-      if (e == hipSuccess && k == 0) a = cand[order[k]];
-      else if (e == hipSuccess && k == 1) b = cand[order[k]];
-      else (void)hipFree(cand[order[k]]);
+    int ka = 0, kb = 1;
+    if (e == hipSuccess) e = rank_pair(cand, sz, st, true, rate, ka, kb);
+    for (int k = 0; k < (int)cand.size(); ++k) {
+      if (e == hipSuccess && k == ka) a = cand[k];
+      else if (e == hipSuccess && k == kb) b = cand[k];
+      else (void)hipFree(cand[k]);
     }
     if (e == hipSuccess && (!a || !b)) e = hipErrorOutOfMemory;
   }
