@@ -414,8 +414,15 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   // LBM_TUNE_XCD_RUN 0 (auto): round robin (runs of one block) for the 4-cell chunk lists whose
   // rows run along y -- the pipe, C3: 184 -> 176 us per step in rocprof, where LDC 256^3 and
   // 512^3 run 9% / 4% slower that way (profiles/r05p_c3_posts_xcd_rocprof.log,
-  // r05_xcd_run_ab.log) -- one contiguous eighth per XCD elsewhere; 17: eighths everywhere
-  a.xcd_run = c->xcd_run == 17 ? 0 : c->xcd_run > 0 ? c->xcd_run : (c->L.swap && !r.quarter && !r.groups) ? 1 : 0;
+  // r05_xcd_run_ab.log); runs of four blocks for compact one-cell ranges of several rounds of
+  // waves -- the coronary tree: 31.1 -> 29.8 us, where one-round C4 runs slower interleaved
+  // (r05_c1_xcd_ab.log, r05z_coronary_xcd_ab.log); one contiguous eighth per XCD elsewhere; 17:
+  // eighths everywhere
+  a.xcd_run = c->xcd_run == 17                               ? 0
+              : c->xcd_run > 0                               ? c->xcd_run
+              : (c->L.swap && !r.quarter && !r.groups)       ? 1
+              : (c->compact && r.quarter && !r.one_round)    ? 3
+                                                             : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
   a.groups = r.groups;
   a.ngroups = r.ngroups;

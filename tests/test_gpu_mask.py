@@ -207,18 +207,25 @@ def test_grid_stride_bitwise(gpu, knob, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lattice", ["pipe_y", "ldc"])
+@pytest.mark.parametrize("lattice", ["pipe_y", "ldc", "coronary"])
 def test_xcd_run_bitwise(gpu, knob, lattice):
     """LBM_TUNE_XCD_RUN changes only which XCD takes which chunk workgroup: a pipe with rows along
-    y (round robin by default) and a cavity (one eighth per XCD by default) under both orders and
-    runs of 16 workgroups step bit for bit alike, residual histories included (each partial slot
-    sums the same chunks whatever the order)."""
+    y (round robin by default), a cavity (one eighth per XCD by default) and the coronary tree
+    (compact one-cell waves, runs of four by default) under both orders and runs of 16 workgroups
+    step bit for bit alike, residual histories included (each partial slot sums the same chunks
+    whatever the order)."""
     from lbm_amd import cases
-    knob(gpu.TUNE_CELLS_PER_LANE, 4)
+    if lattice != "coronary":
+        knob(gpu.TUNE_CELLS_PER_LANE, 4)
 
     def run(v):
         with gpu.tuned(gpu.TUNE_XCD_RUN, v):
-            lat = cases.poiseuille(40, 512, 36)[0] if lattice == "pipe_y" else cases.ldc_device(96, 96, 96)
+            if lattice == "pipe_y":
+                lat = cases.poiseuille(40, 512, 36)[0]
+            elif lattice == "ldc":
+                lat = cases.ldc_device(96, 96, 96)
+            else:
+                lat = cases.coronary(cases.coronary_reference_vessel())[0]
         hist = lat.step(9)
         f = lat.f()
         lat.close()
