@@ -88,6 +88,10 @@ def main():
             d = json.loads(line[0][3:])
             d.pop("kernel_src", None)
             res[v].append(d)
+            if os.environ.get("AB_SHOW_PLACEMENT"):  # the kept pair's write rates, GB/s
+                for k, x in d.items():
+                    g, ch = x["placement"]["candidate_write_gbs"], x["placement"]["chosen"]
+                    print(f"  placement {k}: kept {[g[i] for i in ch] if g else []}, best {max(g) if g else None}", flush=True)
             print(f"round {r} {v:16s} " + "  ".join(f"{k} {x['us_step']:.2f}/{x['k_step_us']:.2f}" for k, x in d.items()),
                   flush=True)
     print("median us/step (wall) per case:")
