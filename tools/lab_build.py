@@ -114,6 +114,12 @@ PATCHES = {
     # placement over up to 160 GiB of candidates (15 at 512^3 instead of 6)
     "budget160": [("lbm_ctx.hip", "constexpr size_t kPlacementBudget = (size_t)64 << 30;",
                    "constexpr size_t kPlacementBudget = (size_t)160 << 30;")],
+    # WRONG VALUES (pricing k_nee_fix): every thread returns at once (launch and ramp only)
+    "fix_empty": [("lbm_kernels.hip", "  if (i >= a.n_nee) return;\n  const int64_t c = a.cells[i];",
+                   "  if (i >= 0) return;\n  const int64_t c = a.cells[i];")],
+    # ... without the own-slot loads (the second round trip)
+    "fix_noload": [("lbm_kernels.hip", "  ((f[Qs] = ((nl >> Qs) & 1u) ? dst[fidx(c, Qs)] : 0.0f), ...);",
+                    "  ((f[Qs] = ((nl >> Qs) & 1u) ? 0.5f : 0.0f), ...);")],
     # every 4-cell whole store plain
     "t4_stores": [("lbm_kernels.hip", "    for (int q = 0; q < kQ; ++q) __builtin_nontemporal_store(v[q], reinterpret_cast<f4*>(d + q * kChunk));",
                    "    for (int q = 0; q < kQ; ++q) *reinterpret_cast<f4*>(d + q * kChunk) = v[q];")],
