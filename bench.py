@@ -30,6 +30,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -55,13 +56,47 @@ def start_cpu_baseline(n: int = 512, steps: int = 1, quick: bool = False):
     C2 (LDC 256^3) and C3 (Poiseuille 128 x 512 x 128) fixed-step samples."""
     env = dict(os.environ, OMP_NUM_THREADS="1")
     cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), str(n), str(steps)]
-    return subprocess.Popen(cmd + (["--quick"] if quick else []), env=env, stdout=subprocess.PIPE, text=True)
+    # its own process group: stop_cpu_baseline ends the samples (grandchildren) with it
+    return subprocess.Popen(cmd + (["--quick"] if quick else []), env=env, stdout=subprocess.PIPE, text=True,
+                            start_new_session=True)
+
+
+def stop_cpu_baseline(p):
+    """End the baseline's whole process group (its samples included) if it is still running: the
+    bench failed or gave up waiting."""
+    if p is not None and p.poll() is None:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.wait()
+
+
+SAMPLE_CORES = 5  # oracle/cpu_baseline.py's samples take the highest-numbered allowed cores
+
+
+def pin_away_from_samples():
+    """Keep this process (and the HIP runtime threads it starts later) off the cores the CPU
+    baseline's samples run on, so the GPU measurements' host side does not share them; only when
+    at least four cores remain."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    keep = allowed[:-SAMPLE_CORES]
+    if len(keep) >= 4:
+        os.sched_setaffinity(0, set(keep))
+        return len(keep)
+    return None
 
 
 def finish_cpu_baseline(p, n: int = 512, timeout: float = 900.0):
     """The `cpu_baseline` object from start_cpu_baseline's child: `value` = the bench workload's
     sample (one core), the configs' samples beside it."""
-    out, _ = p.communicate(timeout=timeout)
+    try:
+        out, _ = p.communicate(timeout=timeout)
+    finally:
+        stop_cpu_baseline(p)
     if p.returncode != 0:
         raise SystemExit(f"cpu baseline failed ({p.returncode})")
     r = json.loads(out.strip().splitlines()[-1])
@@ -103,70 +138,102 @@ def pmc_traffic(workload: str):
 
 
 def ldc_line(n: int, steps: int, dev: int, name: str):
-    """LDC n^3 (device-generated cavity) through timed_mlups: wall-clock MLUPS plus k_step's
-    own roofline and, when profiled on these kernels, its measured HBM traffic."""
+    """LDC n^3 (device-generated cavity) through timed_mlups: wall-clock MLUPS plus the step's
+    roofline from HIP events and, when profiled on these kernels, rocprof's k_step time and the
+    measured HBM traffic."""
     return timed_mlups(cases.ldc_device(n, n, n, device=dev), {"mlups": n ** 3}, steps, name=name)
 
 
-def c5_one_gpu(dev: int, steps: int = 10):
-    """The C5 lattice (LDC 512 x 512 x 4096, 1.07 G cells, ~187 GB) as ONE domain on one GPU:
-    what the 8-GPU configuration's total work costs a single MI355X (timed_mlups: k_step's
-    roofline from HIP events, traffic when profiled)."""
-    t = time.perf_counter()
-    lat = cases.ldc_device(512, 512, 4096, device=dev)
-    setup = time.perf_counter() - t
-    out = timed_mlups(lat, {"mlups": 512 * 512 * 4096}, steps, warm=3, name="ldc_512x512x4096 (C5 lattice)")
-    out["setup_s"] = round(setup, 1)
+def c2_line(dev: int, lattices: int = 3, steps: int = 1000):
+    """Config C2 (LDC 256^3, 1000 steps) on `lattices` fresh lattices in turn, each with its own
+    buffer placement: the 1.28-GB population buffers' HBM write rates differ from allocation to
+    allocation, and with them C2's step time.  The line is the median
+    lattice's, with every lattice's step time, wall time and kept buffers' write rates beside it."""
+    name = "ldc_256^3 (C2)"
+    runs = [timed_mlups(cases.ldc_device(256, 256, 256, device=dev), {"mlups": 256 ** 3}, steps, name=name)
+            for _ in range(lattices)]
+    order = sorted(range(lattices), key=lambda i: runs[i]["roofline"]["step_us"])
+    out = dict(runs[order[lattices // 2]])
+    us = [runs[i]["roofline"]["step_us"] for i in order]
+    out["fresh_lattices"] = {
+        "step_us_min_median_max": [us[0], us[lattices // 2], us[-1]],
+        "frac_min_median_max": [round(runs[i]["roofline"]["frac"], 4) for i in (order[0], order[lattices // 2], order[-1])],
+        "per_lattice": [{"step_us": r["roofline"]["step_us"], "ms_per_step": r["ms_per_step"],
+                         "kept_write_gbs": [r["buffer_placement"]["candidate_write_gbs"][k]
+                                            for k in r["buffer_placement"]["chosen"]]
+                         if r["buffer_placement"]["candidate_write_gbs"] else [],
+                         "best_candidate_write_gbs": max(r["buffer_placement"]["candidate_write_gbs"], default=None),
+                         "setup": r["setup"]} for r in runs],
+    }
     return out
 
 
+def c5_one_gpu(dev: int, steps: int = 500):
+    """The C5 lattice (LDC 512 x 512 x 4096, 1.07 G cells, ~187 GB) as ONE domain on one GPU,
+    BASELINE.md's 500 timed steps: what the 8-GPU configuration's total work costs a single
+    MI355X (timed_mlups: the step's roofline from HIP events, traffic when profiled)."""
+    lat = cases.ldc_device(512, 512, 4096, device=dev)
+    return timed_mlups(lat, {"mlups": 512 * 512 * 4096}, steps, warm=3, name="ldc_512x512x4096 (C5 lattice)")
+
+
 def timed_mlups(lat, cells: dict, steps: int, warm: int = 20, name: str = None):
-    """Wall-clock MLUPS over `steps` steps, then k_step's own roofline from HIP events over a
-    second, profiled run: algorithmic bytes (152 B x fluid cells) / mean launch time against 8 TB/s,
-    with the HBM bytes per launch rocprofv3 counted for this lattice (profiles/pmc_traffic.json,
-    tools/pmc_lattices.sh) when present."""
+    """Wall-clock MLUPS over `steps` steps, and the roofline of the same timed steps: HIP events
+    around the timed lbm_step call on the kernels' stream (lbm_profile 2: no per-launch events,
+    whose ~2-us launches would inflate small lattices' kernel times) give the device time per
+    step of ALL its kernels (k_step, k_nee_fix where the lattice has one, the residual), which
+    cannot exceed the wall time per step; frac = algorithmic bytes (152 B x fluid cells) / that
+    time against 8 TB/s.  rocprofv3's per-kernel means for this lattice at these kernels
+    (profiles/pmc_traffic.json, tools/pmc_lattices.sh; fingerprint-checked) split the step into
+    k_step and k_nee_fix, with the HBM bytes per launch it counted."""
     lay = lat.layout()
     shape = lat.launch_shape()
     store = lat.storage()
+    setup = lat.setup_cost()
+    nee = lat.nee_path()
     algo = lat.counts()["algo_bytes_per_step"]
     lat.step(warm, history=False)
     lat.sync()
+    lat.profile(2)
     t = time.perf_counter()
     lat.step(steps, history=False)
     lat.sync()
     dt = time.perf_counter() - t
-    lat.profile(True)
-    lat.step(min(steps, 200), history=False)
     st = lat.stats()
     placement = lat.placement()
     lat.close()
     out = {k: round(v * steps / dt / 1e6, 1) for k, v in cells.items()}
     out["ms_per_step"] = round(dt / steps * 1e3, 5)
+    out["steps"] = steps
     out["rows_along"] = "xy"[lay["row_axis"] - 1]
     out["active_chunks"] = lay["active_chunks"]
     out["cells_per_lane"] = shape["cells_per_lane"]
     out["grid_stride"] = shape["grid_stride"]
     out["lane_fill"] = shape["lane_fill"]
+    out["nee_values"] = nee["path"]
     out["storage"] = {"compact_rows": store["compact"], "cell_slots": store["cells"],
                       "population_bytes": store["bytes"]}
-    kms = st["step_kernel_ms"] / max(1, st["step_kernel_launches"])
-    if kms > 0:
-        gbs = algo / (kms * 1e-3) / 1e9
-        rl = {"avg_kernel_us": round(kms * 1e3, 2), "algo_bytes_per_launch": int(algo),
-              "achieved": round(gbs, 1), "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None}
-        pmc = pmc_traffic(name) if name else None
-        if pmc and "stale" in pmc:
-            rl["traffic_stale"] = f"profiles/pmc_traffic.json ({pmc['stale']}) was measured on other kernels"
-        elif pmc:
-            rl["traffic"] = pmc["bytes_per_launch"]
-            rl["traffic_over_algo"] = pmc.get("traffic_over_algo")
-            rl["traffic_source"] = f"profiles/pmc_traffic.json ({pmc.get('tag')}, tools/pmc_lattices.sh)"
-        out["roofline"] = rl
-    # where the time of a two-buffer lattice goes: k_step by the buffer it reads (the other one
-    # is written), next to the write rates buffer_placement measured for its candidates
-    out["step_kernel_us_by_source_buffer"] = [
-        round(st[f"step_kernel_src{b}_ms"] / max(1, st[f"step_kernel_src{b}_launches"]) * 1e3, 2) for b in (0, 1)]
+    step_us = st["span_ms"] / max(1, st["span_launches"]) * 1e3
+    gbs = algo / (step_us * 1e-6) / 1e9
+    rl = {"step_us": round(step_us, 3), "algo_bytes_per_step": int(algo), "achieved": round(gbs, 1), "unit": "GB/s",
+          "frac": round(gbs / HBM_PEAK_GBS, 4),
+          "basis": "per step: all kernels of the timed steps between two HIP events on their stream (lbm_profile 2)",
+          "traffic": None}
+    pmc = pmc_traffic(name) if name else None
+    if pmc and "stale" in pmc:
+        rl["rocprof_stale"] = f"profiles/pmc_traffic.json ({pmc['stale']}) was measured on other kernels"
+    elif pmc:
+        k_us, fix_us = pmc.get("k_step_avg_us"), pmc.get("k_nee_fix_avg_us") or 0.0
+        if k_us:
+            rl["rocprof"] = {"k_step_us": k_us, "k_nee_fix_us": fix_us or None,
+                             "frac_k_step": round(algo / (k_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                             "frac_k_step_plus_nee_fix": round(algo / ((k_us + fix_us) * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                             "source": f"profiles/pmc_traffic.json ({pmc.get('tag')}: rocprofv3 --kernel-trace, "
+                                       f"tools/pmc_lattices.sh, another process)"}
+        rl["traffic"] = pmc.get("bytes_per_launch")
+        rl["traffic_over_algo"] = pmc.get("traffic_over_algo")
+    out["roofline"] = rl
     out["buffer_placement"] = placement
+    out["setup"] = setup
     return out
 
 
@@ -362,22 +429,30 @@ def main():
     args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args.gpus, sys.argv[1:]))
-    _imports()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    lbm_amd.require_gpu()
-    torch.cuda.set_device(local)
-    if world > 1:
-        # host-side coordination only (gloo); the data path is liblbm's own RCCL communicator
-        dist.init_process_group("gloo")
+    # the CPU baseline runs on its own host cores while the GPU is measured (N = 1 only); this
+    # process -- and every thread the HIP runtime starts from it -- keeps to the other cores
+    cpu_proc = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu_proc = start_cpu_baseline()
+        pin_away_from_samples()
+    try:
+        _imports()
+        lbm_amd.require_gpu()
+        torch.cuda.set_device(local)
+        if world > 1:
+            # host-side coordination only (gloo); the data path is liblbm's own RCCL communicator
+            dist.init_process_group("gloo")
+        run(args, world, rank, local, args.n, args.n * world, cpu_proc)
+    finally:
+        stop_cpu_baseline(cpu_proc)
 
-    n = args.n
-    nzg = n * world
-    # the CPU baseline runs on its own host cores while the GPU is measured (N = 1 only)
-    cpu_proc = start_cpu_baseline() if world == 1 and not args.no_cpu_baseline else None
+
+def run(args, world, rank, local, n, nzg, cpu_proc):
     lat = cases.ldc_device(n, n, n, z_offset=rank * n, nz_global=nzg, device=local)
     single_ms = None
     if world > 1:
@@ -425,6 +500,7 @@ def main():
     parity_ms = [round(st[f"step_kernel_src{b}_ms"] / max(1, st[f"step_kernel_src{b}_launches"]), 4) for b in (0, 1)]
     placement = lat.placement()
     launch_shape = lat.launch_shape()
+    setup = lat.setup_cost()
     lat.close()
 
     # attainable streaming bandwidth of this device, same run (context for roofline.frac:
@@ -505,6 +581,9 @@ def main():
         "reference_published": {"mlups": 391.86, "config": "LDC 64^3 on GTX 1050 Ti (thesis 4.9.1)"},
         "step_kernel_ms_by_source_buffer": parity_ms,
         "buffer_placement": placement,
+        # lbm_create's cost: wall seconds (placement probe included), the device memory the context
+        # holds, and the most it held while the placement candidates were allocated
+        "setup": setup,
         "launch_shape": launch_shape,
         "residual_last": state["residual"],
         "kernel_src": lbm_amd.kernel_fingerprint(),
@@ -513,7 +592,7 @@ def main():
         line["multi_gpu"] = multi_gpu_block(every, ms_step)
     if world == 1 and not args.no_secondary:
         line["secondary"] = {"ldc_64^3 (published config)": ldc_line(64, 2000, local, "ldc_64^3"),
-                             "ldc_256^3 (C2)": ldc_line(256, 1000, local, "ldc_256^3 (C2)"),
+                             "ldc_256^3 (C2)": c2_line(local),
                              f"ldc{n}_random_velocity_start": perturbed_mlups(n, 50, local),
                              "ldc_512x512x4096 (C5 lattice, single domain)": c5_one_gpu(local),
                              **config_lines(local)}

@@ -297,8 +297,13 @@ int lbm_get_geo(lbm_ctx* ctx, int8_t* geo);
  * (152 B per fluid cell: 19 fp32 loads + 19 fp32 stores). */
 int lbm_get_counts(lbm_ctx* ctx, int64_t* n_box, int64_t* n_fluid, double* algo_bytes_per_step);
 
-/* Kernel timing: when enabled, HIP events bracket every step-kernel launch on the stream it
- * runs on; lbm_stats returns the summed kernel milliseconds and launch count since enabling. */
+/* Kernel timing: enabled = 1: HIP events bracket every step-kernel launch on the stream it
+ * runs on; lbm_stats returns the summed kernel milliseconds and launch count since enabling.
+ * enabled = 2 (spans): no per-launch events (each costs a small launch ~2 us), but one event pair
+ * around all the work each lbm_step call enqueues, on the compute stream: lbm_kernel_times kind 7
+ * returns their milliseconds and the steps they cover -- the device time per step of every kernel
+ * of a step (the step kernel, k_nee_fix, the reductions), which cannot exceed the wall time.
+ * 0 disables.  Enabling resets the sums. */
 int lbm_profile(lbm_ctx* ctx, int enabled);
 int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_bytes);
 /* The same for one kind of launch: kind 0 = the step kernel (k_step: stream-collide with
@@ -306,7 +311,8 @@ int lbm_stats(lbm_ctx* ctx, double* kernel_ms, int64_t* launches, double* algo_b
  * those of its launches that read population buffer 0 / 1 (the A-B parity); slabs with RCCL:
  * 3 = the edge-plane launches, 4 = the interior launches, 5 = the halo exchange on the
  * communication stream (pack, send/recv, unpack), 6 = how long each step's halo outlasted its
- * interior launch (clipped at 0: the part of the exchange not hidden; launches = steps). */
+ * interior launch (clipped at 0: the part of the exchange not hidden; launches = steps);
+ * 7 = lbm_profile(ctx, 2)'s spans (launches = the steps the lbm_step calls asked for). */
 int lbm_kernel_times(lbm_ctx* ctx, int kind, double* ms, int64_t* launches);
 /* Arithmetic of the relaxation's division by tau (the reference divides, ldc.cu:326-363):
  * fast_div = 1 when the 3-instruction correctly rounded quotient is in use (tau verified
@@ -319,9 +325,12 @@ int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
 /* Placement of the two population buffers (not a reference interface).  HBM write bandwidth
  * differs between allocations (~5.5 vs ~6.4 TB/s for 10-GB buffers on MI355X, stable per
  * allocation); when a buffer is larger than 256 MB (the MALL) and the device has room,
- * lbm_create allocates up to sixteen candidates (at most 160 GiB together: 15 at 512^3), times
- * one full-buffer write sweep of each and, of the four fastest, keeps the pair whose tile copies
- * both ways take the least time together (LBM_TUNE_BUFFER_ALLOC).  gbs[0..cap) receives the
+ * lbm_create allocates up to sixteen candidates, times one full-buffer write sweep of each and,
+ * of the four fastest, keeps the pair whose tile copies both ways take the least time together
+ * (LBM_TUNE_BUFFER_ALLOC).  The candidates are held together for the duration of the probe:
+ * lbm_create may TRANSIENTLY allocate up to 160 GiB of device memory (sixteen 10.2-GB
+ * candidates at 512^3), never more than three quarters of the memory free when it starts; the
+ * rest is freed before it returns (lbm_get_setup_cost reports the low point).  gbs[0..cap) receives the
  * candidates' rates (GB/s) in allocation order, *n their count (0: buffers of at most 256 MB,
  * or compact rows, not probed), chosen[2] the indices kept.  Nullable outputs. */
 int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen);
@@ -342,6 +351,18 @@ int lbm_get_launch_shape(lbm_ctx* ctx, int* cells_per_lane, int* main_blocks, in
 /* Fluid cells next to a non-equilibrium-extrapolation boundary (each stores its NEE
  * neighbours' values, producer side). */
 int lbm_get_boundary_cells(lbm_ctx* ctx, int64_t* n_boundary);
+/* How the whole-domain step produces its NEE values (diagnostics, LBM_TUNE_NEE_FIX): path 0 = in
+ * the one-cell waves (or no NEE cell), 1 = NEE blocks in the step launch, 2 = k_nee_fix after it
+ * from (rho, u) records the chunk waves store, one 16-B slot per NEE-adjacent cell, 3 = NEE
+ * records carried into the next step's pulls; max_records = the most records one chunk holds
+ * (path 3; at most 8).  Nullable outputs. */
+int lbm_get_nee_path(lbm_ctx* ctx, int* path, int* max_records);
+/* What lbm_create cost (not a reference interface): create_s = its wall seconds (buffer
+ * placement included); device_bytes = the device memory the context holds after it, and
+ * peak_bytes = the most it held during it (the placement candidates), both as the drops in
+ * hipMemGetInfo's free memory since its start (so other users of the device in the meantime
+ * count too).  Nullable outputs. */
+int lbm_get_setup_cost(lbm_ctx* ctx, double* create_s, int64_t* device_bytes, int64_t* peak_bytes);
 /* Population storage (not a reference interface): compact = 1 when the lattice is stored in
  * compact rows (LBM_TUNE_COMPACT), cells = cell slots per population buffer (the padded box, or
  * the compact rows' spans), bytes = both population buffers' device bytes.  Nullable outputs. */

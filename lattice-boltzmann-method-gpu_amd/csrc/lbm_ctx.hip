@@ -48,7 +48,8 @@ enum : int {
   kKindMid = 4,        // slab step: the interior launch
   kKindHalo = 5,       // slab step: halo pack -> send/recv -> unpack on the communication stream
   kKindExposed = 6,    // slab step: halo end after interior end (clipped at 0): the exchange not hidden
-  kKinds = 7
+  kKindSpan = 7,       // lbm_profile(ctx, 2): one event pair around each lbm_step call's work (launches = steps)
+  kKinds = 8
 };
 
 struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) with their work lists
@@ -67,6 +68,9 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   // step launch, from those records and the cells' own post-collision slots (cells, cell_nl and
   // nee_bc are its list)
   bool nee_fix = false;
+  int* nee_mac_base = nullptr;  // nee_fix: per work unit (chunk-list entry, 64-entry group-list slice), the
+                                // nee_mac slot of its first NEE-adjacent cell (MainArgs::nee_mac_base)
+  int* cell_mac = nullptr;      // nee_fix: per NEE-list entry, its nee_mac slot
   // single-domain chunk-list ranges with nee_chunks (LBM_TUNE_NEE_FIX 2): NEE records instead --
   // the chunk waves compute the NEE values after their relaxation into lbm_ctx::nee_val and put
   // them into the next step's pulls (MainArgs::nee_rec); per chunk-list entry the first record
@@ -75,6 +79,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   int* nee_rec_base = nullptr;
   float4* nee_rec = nullptr;
   int n_rec = 0;
+  int nee_rec_max = 0;  // the most records one chunk holds
   // one-cell ranges whose waves all fit on the device at once: the fused residual's blocks go
   // last (MainArgs::red_last), so that no chunk wave waits for a slot behind them (LDC 64^3
   // 11.30 -> 11.14 us, C4 8.48 -> 8.27 us; a grid of several rounds -- the coronary tree 36.0 ->
@@ -114,7 +119,7 @@ struct lbm_ctx {
   int8_t* codes = nullptr;               // reference codes per storage cell (lbm_get_geo)
   float *bc_in = nullptr, *bc_out = nullptr;  // inlet / outlet u_y tables (lbm_init_case)
   float *rho = nullptr, *ux = nullptr, *uy = nullptr, *uz = nullptr;
-  float4* nee_mac = nullptr;  // whole.nee_fix: (rho, u) of the NEE-adjacent cells, per (compact) cell
+  float4* nee_mac = nullptr;  // whole.nee_fix: (rho, u) of the NEE-adjacent cells, one slot each (storage order)
   // whole.nee_records: the NEE values by step parity (2 x n_rec x 8 floats), and whether the NEE
   // cells' slots of the two buffers miss them (steps since the last materialize_nee)
   float* nee_val = nullptr;
@@ -142,8 +147,9 @@ struct lbm_ctx {
   float tau = 0.f, omc = 0.f;
   bool fast_div = false;  // tau verified for the 3-VALU correctly rounded division
   unsigned long long* retried = nullptr;  // device: 4-cell waves that took the exact division
-  // profiling
+  // profiling: prof = per-launch events (lbm_profile 1); span = one event pair per lbm_step call (2)
   bool prof = false;
+  bool span = false;
   // recorded event pairs, each counted under up to three kinds (lbm_kernel_times)
   struct Rec {
     hipEvent_t a, b;
@@ -211,6 +217,12 @@ struct lbm_ctx {
   // Every producer-side reader -- the RCCL slab step, lbm_group_step, the lazy macros of a
   // producer-side context -- first restores them (prime_walls).
   bool walls_stale = false;
+  // set-up cost (lbm_get_setup_cost): wall seconds of lbm_create, and the device memory it took
+  // (free memory hipMemGetInfo reported at its start, less that at its end / at the lowest point:
+  // the placement probe's candidates)
+  double create_s = 0.0;
+  int64_t mem_resident = 0, mem_peak = 0;
+  size_t mem_free0 = 0, mem_free_min = 0;
   std::string err;
 };
 
@@ -417,8 +429,9 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   // r05_xcd_run_ab.log); runs of four blocks for compact one-cell ranges of several rounds of
   // waves -- the coronary tree: 31.1 -> 29.8 us, where one-round C4 runs slower interleaved
   // (r05_c1_xcd_ab.log, r05z_coronary_xcd_ab.log); one contiguous eighth per XCD elsewhere; 17:
-  // eighths everywhere
-  a.xcd_run = c->xcd_run == 17                               ? 0
+  // eighths everywhere.  Not for grid-stride ranges: their waves take work by XCD (b & 7) and
+  // round (b >> 3) whatever the order, so a run length would only move their partial slots
+  a.xcd_run = (c->xcd_run == 17 || r.stride)                 ? 0
               : c->xcd_run > 0                               ? c->xcd_run
               : (c->L.swap && !r.quarter && !r.groups)       ? 1
               : (c->compact && r.quarter && !r.one_round)    ? 3
@@ -437,6 +450,8 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
   a.nee_chunks = r.nee_chunks ? 1 : 0;
   a.nee_mac = r.nee_fix ? c->nee_mac : nullptr;
+  a.nee_mac_base = r.nee_mac_base;
+  a.cell_mac = r.cell_mac;
   if (r.nee_records) {
     const int64_t per = (int64_t)r.n_rec * 8;
     a.nee_rec_base = r.nee_rec_base;
@@ -506,6 +521,8 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
   r.c_lo2 = lo2;
   r.c_hi2 = hi2;
   std::vector<int> chunks, cells, cells_in_chunk_order;
+  std::vector<int> nee_list;  // the NEE-adjacent cells in list order (grouped by NEE-link mask)
+  std::vector<int> glist;     // the group list (group-list ranges)
   auto in = [&](int64_t k) { return (k >= lo && k < hi) || (k >= lo2 && k < hi2); };
   // Chunk waves also take the NEE-adjacent cells (nee_chunks) when those mostly share their
   // 4-cell group with other fluid cells -- the pipe's rows along y, vessel trees: each such
@@ -603,6 +620,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       sc[i] = cells[perm[i]];
       snl[i] = nl[perm[i]];
     }
+    nee_list = sc;
     int64_t adj = 0;  // list neighbours that are storage neighbours (their lanes share lines)
     for (size_t i = 1; i < sc.size(); ++i) adj += sc[i] == sc[i - 1] + 1;
     if (sc.size() > 1) contig = (double)adj / (double)(sc.size() - 1);
@@ -744,6 +762,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
           cells_in += nseg;
         }
       r.ngroups = (int64_t)gl.size();
+      glist = gl;
       r.group_fill = gl.empty() ? 1.0 : (double)cells_in / (4.0 * (double)gl.size());
       if (r.ngroups) {
         HIPCK(c, hipMalloc(&r.groups, sizeof(int) * gl.size()));
@@ -843,6 +862,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
         ++k;
       }
       ok &= (int)k - base[i] <= kNeeRecMax;
+      r.nee_rec_max = std::max(r.nee_rec_max, (int)k - base[i]);
     }
     base[r.nchunks] = (int)k;
     if (ok && k == co.size()) {
@@ -864,7 +884,31 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
       HIPCK(c, hipStreamSynchronize(c->s_comp));
       r.nee_records = true;
       r.nee_fix = false;
+    } else {
+      r.nee_rec_max = 0;
     }
+  }
+  // k_nee_fix's (rho, u) records (lbm_ctx::nee_mac): one slot per NEE-adjacent cell in storage
+  // order -- the chunk waves number them from their work unit's first slot (nee_mac_base) and their
+  // cells' ranks in the wave, k_nee_fix by list entry (cell_mac).  cells_in_chunk_order is
+  // ascending: the chunks, and the cells in each, are scanned in storage order
+  if (r.nee_fix) {
+    const std::vector<int>& co = cells_in_chunk_order;
+    for (size_t i = 1; i < co.size(); ++i)
+      if (co[i] <= co[i - 1]) {
+        c->err = "build_range: NEE-adjacent cells out of storage order";
+        return LBM_ERR_STATE;
+      }
+    auto slot_of = [&](int64_t cell) { return (int)(std::lower_bound(co.begin(), co.end(), cell) - co.begin()); };
+    std::vector<int> base, cm(nee_list.size());
+    if (r.groups) {
+      for (int64_t b = 0; b * 64 < r.ngroups; ++b) base.push_back(slot_of(glist[b * 64] & ~3));
+    } else {
+      for (int i = 0; i < r.nchunks; ++i) base.push_back(slot_of((int64_t)chunks[i] * kChunk));
+    }
+    for (size_t i = 0; i < nee_list.size(); ++i) cm[i] = slot_of(nee_list[i]);
+    RCK(upload(c, &r.nee_mac_base, base));
+    RCK(upload(c, &r.cell_mac, cm));
   }
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
@@ -881,6 +925,8 @@ void free_range(Range& r) {
   if (r.cell_row) (void)hipFree(r.cell_row);
   if (r.cell_nl) (void)hipFree(r.cell_nl);
   if (r.nee_rec_base) (void)hipFree(r.nee_rec_base);
+  if (r.nee_mac_base) (void)hipFree(r.nee_mac_base);
+  if (r.cell_mac) (void)hipFree(r.cell_mac);
   if (r.nee_rec) (void)hipFree(r.nee_rec);
   if (r.nee_bc) (void)hipFree(r.nee_bc);
   r = Range{};
@@ -1001,7 +1047,7 @@ int prime_walls(lbm_ctx* c) {
 // buffers >= 1 GiB, so the 647-MB buffers of the C3 pipe took whatever came first); smaller
 // ones (MALL resident, latency-bound) and LBM_TUNE_BUFFER_ALLOC = 1 take the first two
 // allocations (the latter still timed, for A/B).
-// The candidates take at most kPlacementBudget bytes together (15 at 512^3: 3297.7 against
+// The candidates take at most kPlacementBudget bytes together (16 at 512^3: 3297.7 against
 // 3336.6 us per step with the round-4 budget's six, profiles/r05s_placement.log) and number at most
 // kMaxCand: at LDC 256^3 (1.28-GB buffers) one or two of six candidates wrote at ~6.1 TB/s and
 // the rest at 4.9-5.6, so the step that writes the slower kept buffer ran 433 instead of 422 us,
@@ -1070,7 +1116,10 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
     hipError_t e = hipMemGetInfo(&fr, &tot);
     if (e != hipSuccess) return e;
     const size_t need = 2 * bytes + others;
-    const int cap = (int)std::max<size_t>(2, std::min<size_t>(kMaxCand, kPlacementBudget / bytes));
+    // at most kPlacementBudget, and a quarter of the free memory stays free while the candidates
+    // are held (a device shared with other contexts or processes)
+    const size_t budget = std::min(kPlacementBudget, fr / 4 * 3);
+    const int cap = (int)std::max<size_t>(2, std::min<size_t>(kMaxCand, budget / bytes));
     if (fr > need) ncand = (int)std::min<size_t>(cap, 2 + (fr - need) / bytes);
   }
   std::vector<void*> p;
@@ -1088,6 +1137,10 @@ hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
     }
     p.push_back(q);
     e = hipMemsetAsync(q, 0, bytes, c->s_comp);
+  }
+  {  // the set-up's low point of free device memory: every candidate held (lbm_get_setup_cost)
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) c->mem_free_min = std::min(c->mem_free_min, fr);
   }
   if (e == hipSuccess && probe) {
     int ka = 0, kb = 1;
@@ -1348,6 +1401,12 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
   } while (0)
 
   CK(hipSetDevice(d.device));
+  const auto t_create = std::chrono::steady_clock::now();
+  {
+    size_t tot = 0;
+    CK(hipMemGetInfo(&c->mem_free0, &tot));
+    c->mem_free_min = c->mem_free0;
+  }
   CK(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking));
   for (hipEvent_t* e : {&c->ev_edge, &c->ev_halo, &c->ev_mid, &c->ev_fin, &c->ev_sum[0], &c->ev_sum[1]})
@@ -1527,10 +1586,7 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
       CK(hipMalloc(&c->red_part, sizeof(double) * 2 * c->red_n));
     }
     if (c->whole.nee_records) CK(hipMalloc(&c->nee_val, sizeof(float) * 2 * 8 * (size_t)c->whole.n_rec));
-    if (c->whole.nee_fix) {  // per (compact) cell: only the NEE-adjacent cells' entries are used
-      const int64_t n = c->compact ? c->ncell_c : L.ncell;
-      CK(hipMalloc(&c->nee_mac, sizeof(float4) * n));
-    }
+    if (c->whole.nee_fix) CK(hipMalloc(&c->nee_mac, sizeof(float4) * std::max(1, c->whole.n_nee)));  // one per NEE-adjacent cell
     c->edge.part = c->whole.part + c->whole.npart;
     c->mid.part = c->edge.part + c->edge.npart;
   }
@@ -1549,6 +1605,15 @@ int lbm_create(const lbm_desc* desc, lbm_ctx** out) {
     const size_t bytes = sizeof(float) * L.buf_floats();
     CK(buffer_placement(c, bytes, (size_t)1 << 30));
     for (int b = 0; b < 2; ++b) c->buf[b] = c->alloc[b] + L.guard * kQ * kChunk;
+  }
+  {
+    size_t fr = 0, tot = 0;
+    CK(hipStreamSynchronize(c->s_comp));
+    CK(hipMemGetInfo(&fr, &tot));
+    c->mem_free_min = std::min(c->mem_free_min, fr);
+    c->mem_resident = (int64_t)c->mem_free0 - (int64_t)fr;
+    c->mem_peak = (int64_t)c->mem_free0 - (int64_t)c->mem_free_min;
+    c->create_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_create).count();
   }
 #undef CK
   *out = c;
@@ -2068,7 +2133,18 @@ int lbm_step(lbm_ctx* c, int nsteps, float* residual_hist, int* steps_done) {
     RCK(ensure_hist(c, nsteps));
     HIPCK(c, hipMemsetAsync(c->hist, 0xFF, sizeof(float) * nsteps, c->s_comp));  // NaN: step not run
   }
+  hipEvent_t sp0 = nullptr, sp1 = nullptr;
+  if (c->span) {  // everything this call enqueues, between two events on the compute stream
+    RCK(take_event(c, &sp0));
+    RCK(take_event(c, &sp1));
+    HIPCK(c, hipEventRecord(sp0, c->s_comp));
+  }
   RCK(c->comm ? step_rccl(c, nsteps, want_hist) : step_single(c, nsteps, want_hist));
+  if (c->span) {  // (step_rccl ends with the compute stream waiting for the communication stream)
+    HIPCK(c, hipEventRecord(sp1, c->s_comp));
+    c->recs.push_back({sp0, sp1, {kKindSpan, -1, -1}});
+    c->kind_n[kKindSpan] += nsteps;
+  }
   c->macros_stale = true;
   const bool sync = want_hist || steps_done || c->conv_enabled;
   if (sync) {
@@ -2217,6 +2293,36 @@ struct CkptHeader {
   ConvState conv;
 };
 constexpr int32_t kCkptVersion = 3;
+// version 2 (round 4): no walls_stale -- every context then stored its wall slots producer-side
+struct CkptHeaderV2 {
+  char magic[8];
+  int32_t version, nx, ny, nz, z_offset, nz_global, case_kind, swap, pitch, xshift, steps_done, cur;
+  int32_t halo_primed;
+  uint32_t tau_bits;
+  int64_t ncell, buf_floats;
+  ConvState conv;
+};
+// the header of a version-2 or version-3 file as version 3 (false: short read, or another magic);
+// *version receives the file's version
+bool read_ckpt_header(std::FILE* f, CkptHeader& h, int32_t* version) {
+  char head[12];
+  *version = -1;
+  if (std::fread(head, sizeof(head), 1, f) != 1 || std::memcmp(head, "LBMCKPT1", 8) != 0) return false;
+  std::memcpy(version, head + 8, 4);
+  if (std::fseek(f, 0, SEEK_SET) != 0) return false;
+  if (*version == 2) {
+    CkptHeaderV2 o{};
+    if (std::fread(&o, sizeof(o), 1, f) != 1) return false;
+    std::memcpy(h.magic, o.magic, 8);
+    h.version = o.version; h.nx = o.nx; h.ny = o.ny; h.nz = o.nz; h.z_offset = o.z_offset;
+    h.nz_global = o.nz_global; h.case_kind = o.case_kind; h.swap = o.swap; h.pitch = o.pitch;
+    h.xshift = o.xshift; h.steps_done = o.steps_done; h.cur = o.cur; h.halo_primed = o.halo_primed;
+    h.walls_stale = 0;  // written by producer-side steps
+    h.tau_bits = o.tau_bits; h.ncell = o.ncell; h.buf_floats = o.buf_floats; h.conv = o.conv;
+    return true;
+  }
+  return *version == kCkptVersion && std::fread(&h, sizeof(h), 1, f) == 1;
+}
 
 constexpr size_t kCkptSlice = (size_t)64 << 20;  // bytes staged through the host per copy
 
@@ -2278,8 +2384,15 @@ int lbm_checkpoint_load(lbm_ctx* c, const char* path) {
   CkptHeader h{};
   uint32_t tau_bits;
   std::memcpy(&tau_bits, &c->tau, 4);
-  bool match = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, "LBMCKPT1", 8) == 0 && h.version == kCkptVersion &&
-               h.nx == c->L.nx && h.ny == c->L.ny && h.nz == c->L.nz && h.z_offset == c->d.z_offset &&
+  int32_t version = -1;
+  const bool header = read_ckpt_header(f, h, &version);
+  if (!header && version >= 0 && version != 2 && version != kCkptVersion) {
+    std::fclose(f);
+    c->err = std::string("lbm_checkpoint_load: ") + path + ": unsupported checkpoint version " +
+             std::to_string(version) + " (this library reads versions 2 and " + std::to_string(kCkptVersion) + ")";
+    return LBM_ERR_ARG;
+  }
+  bool match = header && h.nx == c->L.nx && h.ny == c->L.ny && h.nz == c->L.nz && h.z_offset == c->d.z_offset &&
                h.nz_global == c->d.nz_global && h.case_kind == c->d.case_kind && h.swap == c->L.swap &&
                h.pitch == c->L.pitch && h.xshift == c->L.xshift && h.tau_bits == tau_bits &&
                h.ncell == (c->compact ? c->ncell_c : c->L.ncell) && h.buf_floats == c->pop_floats();
@@ -2388,6 +2501,22 @@ int lbm_get_storage(lbm_ctx* c, int* compact, int64_t* cells, int64_t* bytes) {
   return LBM_OK;
 }
 
+int lbm_get_nee_path(lbm_ctx* c, int* path, int* max_records) {
+  if (!c) return LBM_ERR_ARG;
+  const Range& r = c->whole;
+  if (path) *path = r.nee_records ? 3 : r.nee_fix ? 2 : r.nee_blocks > 0 ? 1 : 0;
+  if (max_records) *max_records = r.nee_records ? r.nee_rec_max : 0;
+  return LBM_OK;
+}
+
+int lbm_get_setup_cost(lbm_ctx* c, double* create_s, int64_t* device_bytes, int64_t* peak_bytes) {
+  if (!c) return LBM_ERR_ARG;
+  if (create_s) *create_s = c->create_s;
+  if (device_bytes) *device_bytes = c->mem_resident;
+  if (peak_bytes) *peak_bytes = c->mem_peak;
+  return LBM_OK;
+}
+
 int lbm_get_boundary_cells(lbm_ctx* c, int64_t* n_boundary) {
   if (!c || !n_boundary) return LBM_ERR_ARG;
   *n_boundary = c->n_slow;
@@ -2396,8 +2525,10 @@ int lbm_get_boundary_cells(lbm_ctx* c, int64_t* n_boundary) {
 
 int lbm_profile(lbm_ctx* c, int enabled) {
   if (!c) return LBM_ERR_ARG;
+  if (enabled < 0 || enabled > 2) return LBM_ERR_ARG;
   RCK(harvest_profile(c));
-  c->prof = enabled != 0;
+  c->prof = enabled == 1;
+  c->span = enabled == 2;
   c->kernel_ms = 0.0;
   c->launches = 0;
   for (int k = 0; k < kKinds; ++k) {

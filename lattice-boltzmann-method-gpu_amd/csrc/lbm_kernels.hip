@@ -848,12 +848,23 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
     }
   }
   if (a.nee_mac != nullptr && __any(store != 0u && (t4 & kNee4) != 0u)) {  // wave-uniform
-    // the NEE-adjacent cells' (rho, u) of this step for k_nee_fix (one 16-B store per cell)
+    // the NEE-adjacent cells' (rho, u) of this step for k_nee_fix (one 16-B store per cell), at
+    // slots numbered in storage order: the work unit's first slot plus the cell's rank among the
+    // wave's such cells (lanes in storage order, a lane's cells j = 0..3)
     const f4 R{r0, r1, r2, r3};
+    unsigned nm = 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if ((store & (1u << j)) && ((t4 >> (8 * j)) & kNeeAdj))
-        a.nee_mac[c + j] = make_float4(R[j], UX[j], UY[j], UZ[j]);
+      if ((store & (1u << j)) && ((t4 >> (8 * j)) & kNeeAdj)) nm |= 1u << j;
+    int k = a.nee_mac_base[GROUPS ? (int)(cb >> 6) : ridx];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t bj = __ballot((nm >> j) & 1u);
+      k += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj, 0u));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (nm & (1u << j)) a.nee_mac[k++] = make_float4(R[j], UX[j], UY[j], UZ[j]);
   }
   // Whole 16-B stores whenever the lane's other cells may take garbage: passive cells
   // no fluid cell pulls (their macros are masked on read-out).  Wall and NEE cells hold
@@ -1289,7 +1300,7 @@ __global__ __launch_bounds__(64) void k_nee_fix(const MainArgs a) {
   const float4* rec = a.nee_bc + (int64_t)i * kNeeSlots;
   const BcSlots bc = a.bc_uniform ? BcSlots{a.bc_const, a.bc_const, a.bc_const, a.bc_const, a.bc_const}
                                   : BcSlots{rec[0], rec[1], rec[2], rec[3], rec[4]};
-  const float4 m = a.nee_mac[c];
+  const float4 m = a.nee_mac[a.cell_mac[i]];
   float f[kQ];
   own_slots(f, a.dst, c, nl, AllQ{});
   const Pref pre = Pref::exact(m.x);
@@ -1397,7 +1408,7 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
       const int step = (a.main_blocks >> 3) * (WPB);
       for (int i = lo + (b >> 3) * (WPB) + wave; i < hi; i += step) {
         const uint64_t lm = MASK ? a.lane_masks[i] : ~0ull;
-        acc += process_chunk<FAST, SW, MASK>(a, chunk_of(a, i) * kChunk, lane, lm);
+        acc += process_chunk<FAST, SW, MASK>(a, chunk_of(a, i) * kChunk, lane, lm, i);
       }
     } else if (idx < a.nchunks) {
       const uint64_t lm = MASK ? a.lane_masks[idx] : ~0ull;  // uniform, loaded beside the chunk id

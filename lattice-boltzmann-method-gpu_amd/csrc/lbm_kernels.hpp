@@ -133,9 +133,13 @@ struct MainArgs {
   const float* nee_in;
   float* nee_out;
   float4* nee_mac;          // nullable (single-domain nee_chunks ranges, LBM_TUNE_NEE_FIX): the chunk
-                            // waves store each NEE-adjacent cell's (rho, ux, uy, uz) here, indexed by
-                            // cell; k_nee_fix (launch_nee_fix, after the step launch) reads them with
-                            // the cells' own post-collision slots and stores the NEE values
+                            // waves store each NEE-adjacent cell's (rho, ux, uy, uz) here, one slot
+                            // per such cell in storage order; k_nee_fix (launch_nee_fix, after the
+                            // step launch) reads them with the cells' own post-collision slots and
+                            // stores the NEE values
+  const int* nee_mac_base;  // per work unit (chunk-list entry; 64-entry slice of a group list): the
+                            // slot of its first NEE-adjacent cell (prefix counts)
+  const int* cell_mac;      // per NEE-list entry (cells[i]): its nee_mac slot
   int swap;             // 1: storage rows run along physical y (Layout::swap)
   // Compact rows (nullable; sparse single-domain lattices, group lists only): every per-cell
   // array above and the population buffers are indexed by compact cell ids -- storage row

@@ -87,6 +87,7 @@ LBM_SYMBOLS = [
     "lbm_version", "lbm_last_error", "lbm_tune", "lbm_get_nonfinite", "lbm_create", "lbm_destroy", "lbm_init_equilibrium", "lbm_init_ldc",
     "lbm_init_case", "lbm_set_f", "lbm_field_digest", "lbm_set_convergence", "lbm_set_residual_order", "lbm_step", "lbm_sync", "lbm_get_state", "lbm_get_macros", "lbm_get_f",
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_storage", "lbm_get_numerics",
+    "lbm_get_nee_path", "lbm_get_setup_cost",
     "lbm_get_layout", "lbm_get_launch_shape", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
     "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_debug_fail_next_wait", "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
 ]
@@ -183,6 +184,8 @@ def lbm_lib() -> C.CDLL:
             "lbm_kernel_times": (C.c_int, [P, C.c_int, f64p, i64p]),
             "lbm_get_boundary_cells": (C.c_int, [P, i64p]),
             "lbm_get_storage": (C.c_int, [P, ip, i64p, i64p]),
+            "lbm_get_nee_path": (C.c_int, [P, ip, ip]),
+            "lbm_get_setup_cost": (C.c_int, [P, f64p, i64p, i64p]),
             "lbm_checkpoint_save": (C.c_int, [P, C.c_char_p]),
             "lbm_checkpoint_load": (C.c_int, [P, C.c_char_p]),
             "lbm_get_numerics": (C.c_int, [P, ip, i64p]),
@@ -574,6 +577,20 @@ class Lattice:
         self._ck(lbm_lib().lbm_get_storage(self.h, C.byref(cm), C.byref(cells), C.byref(by)), "lbm_get_storage")
         return {"compact": bool(cm.value), "cells": cells.value, "bytes": by.value}
 
+    def nee_path(self):
+        """How the step produces its NEE values (lbm_get_nee_path): "cells" (one-cell waves or
+        none), "blocks", "fix" (k_nee_fix) or "records", and the most records one chunk holds."""
+        p, m = C.c_int(), C.c_int()
+        self._ck(lbm_lib().lbm_get_nee_path(self.h, C.byref(p), C.byref(m)), "lbm_get_nee_path")
+        return {"path": ("cells", "blocks", "fix", "records")[p.value], "max_records": m.value}
+
+    def setup_cost(self):
+        """lbm_create's wall seconds, the device bytes the context holds and the most it held
+        during creation (placement candidates), from hipMemGetInfo (lbm_get_setup_cost)."""
+        s, b, pk = C.c_double(), C.c_int64(), C.c_int64()
+        self._ck(lbm_lib().lbm_get_setup_cost(self.h, C.byref(s), C.byref(b), C.byref(pk)), "lbm_get_setup_cost")
+        return {"create_s": round(s.value, 3), "device_bytes": b.value, "peak_bytes": pk.value}
+
     def launch_shape(self):
         """How the step kernel covers the chunks: cells per lane, chunk workgroups, whether they
         loop over their XCD's chunks (grid stride), mean share of busy chunk lanes."""
@@ -596,15 +613,18 @@ class Lattice:
         self._ck(lbm_lib().lbm_buffer_placement(self.h, gbs, 16, C.byref(n), ch), "lbm_buffer_placement")
         return {"candidate_write_gbs": [round(gbs[i], 1) for i in range(min(n.value, 16))], "chosen": [ch[0], ch[1]]}
 
-    def profile(self, enabled: bool = True):
-        self._ck(lbm_lib().lbm_profile(self.h, 1 if enabled else 0), "lbm_profile")
+    def profile(self, enabled=True):
+        """lbm_profile: True / 1 per-launch HIP events, 2 one event pair per lbm_step call
+        (spans: stats()["span_ms"] over stats()["span_launches"] steps), False / 0 off."""
+        mode = 1 if enabled is True else 0 if enabled is False else int(enabled)
+        self._ck(lbm_lib().lbm_profile(self.h, mode), "lbm_profile")
 
     def stats(self):
         ms, n, by = C.c_double(), C.c_int64(), C.c_double()
         self._ck(lbm_lib().lbm_stats(self.h, C.byref(ms), C.byref(n), C.byref(by)), "lbm_stats")
         out = {"kernel_ms": ms.value, "launches": n.value, "algo_bytes": by.value}
         for kind, name in ((0, "step_kernel"), (1, "step_kernel_src0"), (2, "step_kernel_src1"), (3, "edge"),
-                           (4, "interior"), (5, "halo"), (6, "halo_exposed")):
+                           (4, "interior"), (5, "halo"), (6, "halo_exposed"), (7, "span")):
             m, k = C.c_double(), C.c_int64()
             self._ck(lbm_lib().lbm_kernel_times(self.h, kind, C.byref(m), C.byref(k)), "lbm_kernel_times")
             out[name + "_ms"], out[name + "_launches"] = m.value, k.value

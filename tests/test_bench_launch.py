@@ -138,3 +138,25 @@ def test_cpu_baseline_assembly():
     assert "LDC 24^3" in line["sample"] and "3 step(s)" in line["sample"]
     assert line["c1"]["steps"] == 200 and line["c1"]["mlups"] > 0
     assert "c2" not in line and "c1_converge" not in line  # --quick
+
+
+def test_cpu_baseline_group_is_stopped():
+    """A bench that fails (or gives up waiting) ends the CPU baseline's whole process group: the
+    child and the sample processes it started."""
+    import time
+    b = _bench()
+    p = b.start_cpu_baseline(96, 50, quick=True)  # several seconds of oracle work per sample
+    time.sleep(2.0)
+    pgid = os.getpgid(p.pid)
+    assert pgid == p.pid  # its own session / group
+    b.stop_cpu_baseline(p)
+    assert p.returncode is not None
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        try:
+            os.killpg(pgid, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("baseline samples still running")

@@ -212,6 +212,46 @@ def test_load_rejects_corrupt_header(gpu, tmp_path):
     a.close()
 
 
+def _as_version2(v3: bytes) -> bytes:
+    """A version-3 file of a producer-side context rewritten in round 4's version-2 layout:
+    the header without walls_stale (CkptHeader: magic[8], 12 int32 from version to cur,
+    halo_primed, walls_stale, tau_bits, 4 B padding, int64 ncell, buf_floats, ConvState (72 B);
+    version 2: halo_primed, tau_bits, then the int64s at once)."""
+    import struct
+    assert struct.unpack_from("<i", v3, 60)[0] == 0  # walls_stale: producer side
+    body = v3[160:]
+    return v3[:8] + struct.pack("<i", 2) + v3[12:60] + v3[64:68] + v3[72:160] + body
+
+
+def test_load_version2_file(gpu, tmp_path):
+    """Round 4's checkpoint format (version 2, no walls_stale field) still loads: as a file whose
+    wall slots were written by the steps, and the resumed run continues bit for bit.  Any other
+    version is refused by number."""
+    import struct
+    from lbm_amd import cases, LbmError
+    a = cases.poiseuille(20, 28, 20)[0]
+    a.step(7)
+    p3 = tmp_path / "v3.bin"
+    a.checkpoint_save(str(p3))
+    ha = a.step(12)
+    raw = p3.read_bytes()
+    p2 = tmp_path / "v2.bin"
+    p2.write_bytes(_as_version2(raw))
+    b = cases.poiseuille(20, 28, 20)[0]
+    b.checkpoint_load(str(p2))
+    hb = b.step(12)
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32))
+    assert np.array_equal(a.f().view(np.uint32), b.f().view(np.uint32))
+    bad = bytearray(raw)
+    struct.pack_into("<i", bad, 8, 9)
+    p9 = tmp_path / "v9.bin"
+    p9.write_bytes(bytes(bad))
+    with pytest.raises(LbmError, match="unsupported checkpoint version 9"):
+        b.checkpoint_load(str(p9))
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("save_box,load_box", [(0, 1), (1, 0)], ids=["consumer_to_producer", "producer_to_consumer"])
 @pytest.mark.parametrize("steps", [1, 7])
 def test_resume_across_bounce_back_modes(gpu, tmp_path, knob, save_box, load_box, steps):

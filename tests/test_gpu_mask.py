@@ -207,21 +207,26 @@ def test_grid_stride_bitwise(gpu, knob, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lattice", ["pipe_y", "ldc", "coronary"])
+@pytest.mark.parametrize("lattice", ["pipe_y", "pipe_y_stride", "ldc", "coronary"])
 def test_xcd_run_bitwise(gpu, knob, lattice):
     """LBM_TUNE_XCD_RUN changes only which XCD takes which chunk workgroup: a pipe with rows along
     y (round robin by default), a cavity (one eighth per XCD by default) and the coronary tree
     (compact one-cell waves, runs of four by default) under both orders and runs of 16 workgroups
     step bit for bit alike, residual histories included (each partial slot sums the same chunks
-    whatever the order)."""
+    whatever the order).  The pipe's grid-stride loop (LBM_TUNE_GRID_STRIDE 2), whose waves take
+    their chunks by XCD and round whatever the order, ignores the knob: same partial slots, same
+    residual bits."""
     from lbm_amd import cases
     if lattice != "coronary":
         knob(gpu.TUNE_CELLS_PER_LANE, 4)
+    if lattice == "pipe_y_stride":
+        knob(gpu.TUNE_GRID_STRIDE, 2)
 
     def run(v):
         with gpu.tuned(gpu.TUNE_XCD_RUN, v):
-            if lattice == "pipe_y":
+            if lattice.startswith("pipe_y"):
                 lat = cases.poiseuille(40, 512, 36)[0]
+                assert lat.launch_shape()["grid_stride"] == (1 if lattice == "pipe_y_stride" else 0)
             elif lattice == "ldc":
                 lat = cases.ldc_device(96, 96, 96)
             else:

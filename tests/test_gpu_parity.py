@@ -476,6 +476,30 @@ def test_poiseuille_nee_paths_bitwise(gpu, oracle, knob, nee_fix, shape):
     assert_bitwise(lat, o, geo, 1, f"pipe {shape} stopped at 46")
 
 
+@pytest.mark.parametrize("shape,most", [((32, 32, 32), 8), ((37, 29, 23), 8), ((13, 45, 11), 6)])
+def test_nee_records_full_chunks_bitwise(gpu, oracle, knob, shape, most):
+    """NEE records (LBM_TUNE_NEE_FIX 2) on chunks holding up to eight records: the cavity with rows
+    along y puts one lid-adjacent cell at the end of every row, so a 256-cell chunk of 32-cell rows
+    holds eight.  Their static records are 8 x 9 = 72 float4, more than one 64-lane wave-load; in
+    round 5 a single wave-load left the ninth float4 onward unloaded (LDC 32^3, 840 of 21,952 fluid
+    cells wrong at step 3).  Bit for bit against the oracle, with the ragged
+    shapes' padded rows (pitch 32 for 29 cells; 48 for 45: five or six rows per chunk)."""
+    from lbm_amd import cases
+    import lbm_amd
+    knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)
+    knob(lbm_amd.TUNE_ROW_AXIS, 2)
+    knob(lbm_amd.TUNE_NEE_FIX, 2)
+    nx, ny, nz = shape
+    lat, geo = cases.ldc(nx, ny, nz)
+    assert lat.layout()["row_axis"] == 2
+    assert lat.nee_path() == {"path": "records", "max_records": most}, lat.nee_path()
+    o = fp64_sum(oracle.Oracle(oracle.LDC, geo, 0.55, ldc_order=oracle.TWO_PHASE))
+    for s in (1, 2, 3, 40):
+        hg, ho = lat.step(s), o.step(s)
+        assert_bitwise(lat, o, geo, 0, f"ldc {shape} records +{s}")
+        assert_residuals(hg, ho)
+
+
 def test_north_star_512_bitwise(gpu, oracle):
     """The north-star lattice itself (LDC 512^3, the bench's N = 1 workload, generated on the
     device as bench.py does) against the oracle on the host: (rho, u) bit for bit on all
