@@ -476,14 +476,16 @@ def test_poiseuille_nee_paths_bitwise(gpu, oracle, knob, nee_fix, shape):
     assert_bitwise(lat, o, geo, 1, f"pipe {shape} stopped at 46")
 
 
-@pytest.mark.parametrize("shape,most", [((32, 32, 32), 8), ((37, 29, 23), 8), ((13, 45, 11), 6)])
+@pytest.mark.parametrize("shape,most", [((32, 32, 32), 8), ((37, 30, 23), 8), ((13, 47, 11), 6)])
 def test_nee_records_full_chunks_bitwise(gpu, oracle, knob, shape, most):
     """NEE records (LBM_TUNE_NEE_FIX 2) on chunks holding up to eight records: the cavity with rows
     along y puts one lid-adjacent cell at the end of every row, so a 256-cell chunk of 32-cell rows
     holds eight.  Their static records are 8 x 9 = 72 float4, more than one 64-lane wave-load; in
     round 5 a single wave-load left the ninth float4 onward unloaded (LDC 32^3, 840 of 21,952 fluid
     cells wrong at step 3).  Bit for bit against the oracle, with the ragged
-    shapes' padded rows (pitch 32 for 29 cells; 48 for 45: five or six rows per chunk)."""
+    shapes' padded rows (pitch 32 for 30 cells; 48 for 47: five or six rows per chunk).  Records
+    need the chunk waves to collide the lid-adjacent cells (nee_chunks), so the row lengths put
+    that cell in a 4-cell group with other fluid cells (ny - 5 not a multiple of 4)."""
     from lbm_amd import cases
     import lbm_amd
     knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)

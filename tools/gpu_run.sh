@@ -3,7 +3,7 @@
 #   /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_run.sh <tag> <step>[,<step>...]
 # Steps, in the order given; each under its own time limit, and the session stops at the first
 # step that fails (a GPU fault, abort, segfault or time limit ends it: nothing more runs):
-#   tests      pytest -m gpu (TESTS="-k expr" narrows it)            -> <tag>/tests.txt
+#   tests      pytest -m gpu (TEST_PATHS="tests/a.py tests/b.py::test_x" narrows it) -> <tag>/tests.txt
 #   smoke      __graft_entry__.smoke()                              -> <tag>/smoke.txt
 #   bench      python bench.py $BENCH_ARGS (default: the driver's)  -> <tag>/bench.json
 #   spread     BENCH_RUNS fresh headline-only bench processes       -> <tag>/bench_spread.jsonl
@@ -29,7 +29,7 @@ run() {  # run <seconds> <log> <cmd...>
 }
 for s in ${steps//,/ }; do
   case $s in
-    tests) run 900 "$out/tests.txt" python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:-} ;;
+    tests) run 900 "$out/tests.txt" python3 -u -m pytest ${TEST_PATHS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) run 300 "$out/smoke.txt" python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run 900 "$out/bench.json" python3 -u bench.py ${BENCH_ARGS:-} ;;
     spread)
