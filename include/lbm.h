@@ -202,22 +202,24 @@ typedef enum {
                                    one-cell single-domain range bounces back on the consumer side;
                                    1 they load them like any lattice's */
   LBM_TUNE_NEE_FIX = 12,        /* NEE values of a single-domain 4-cell range whose chunk waves collide
-                                   its NEE-adjacent cells (the pipe's rows along y): 0 (default) one
-                                   small launch after the step kernel stores them from the cells'
-                                   (rho, u) the chunk waves recorded and their own post-collision
-                                   slots; 1 NEE blocks in the step launch re-pull and re-collide
-                                   every NEE-adjacent cell (round 4); 2 NEE records -- a chunk wave
-                                   computes them after its relaxation into a 32-B record per cell,
-                                   and the next step's wave puts them into its pulls (chunk lists
-                                   of the dense box with at most 8 such cells per chunk; otherwise
-                                   as 0) */
+                                   its NEE-adjacent cells (the pipe's rows along y): 0 (default) and
+                                   1 NEE blocks in the step launch re-pull and re-collide every
+                                   NEE-adjacent cell; 3 one small launch after the step kernel
+                                   (k_nee_fix) stores them from the cells' (rho, u) the chunk waves
+                                   recorded and their own post-collision slots (round 5's default);
+                                   2 NEE records -- a chunk wave computes them after its relaxation
+                                   into a 32-B record per cell, and the next step's wave puts them
+                                   into its pulls (chunk lists of the dense box with at most 8 such
+                                   cells per chunk; otherwise as 3) */
   LBM_TUNE_XCD_RUN = 13,        /* order of the step kernel's chunk workgroups over the 8 XCDs: 0
                                    (default) round robin (as L = 1) for 4-cell chunk lists whose rows
                                    run along y (the pipe), runs of four (L = 3) for compact one-cell
                                    ranges of several rounds of waves (vessel trees), one contiguous
                                    eighth of the chunks per XCD elsewhere; L = 1..16 runs of 2^(L-1) workgroups, XCD x taking
                                    runs x, x + 8, x + 16, ...; 17 one eighth per XCD everywhere */
-  LBM_TUNE_COUNT = 14
+  LBM_TUNE_BLOCK_WAVES = 14,    /* workgroup size of the 4-cell chunk-list kernel (dense box, no NEE
+                                   records): 0 (default) and 4 four waves, 2 two waves */
+  LBM_TUNE_COUNT = 15
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

@@ -320,7 +320,7 @@ def test_group_step_after_consumer_side_steps(gpu):
     b.close()
 
 
-@pytest.mark.parametrize("modes", [(2, 2), (2, 1), (1, 2), (2, 0)], ids=["rec_rec", "rec_blocks", "blocks_rec", "rec_fix"])
+@pytest.mark.parametrize("modes", [(2, 2), (2, 1), (1, 2), (2, 3)], ids=["rec_rec", "rec_blocks", "blocks_rec", "rec_fix"])
 def test_resume_nee_records(gpu, tmp_path, knob, modes):
     """A pipe whose NEE values travel as NEE records (LBM_TUNE_NEE_FIX 2: the NEE cells' slots are
     never written while stepping): the file holds the values in those slots (save puts them

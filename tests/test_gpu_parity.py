@@ -446,12 +446,12 @@ def test_poiseuille_c3_full_size_bitwise(gpu, oracle):
     assert o.bad_reads() == 0
 
 
-@pytest.mark.parametrize("nee_fix", [0, 1, 2], ids=["nee_fix", "nee_blocks", "nee_records"])
+@pytest.mark.parametrize("nee_fix", [3, 1, 2], ids=["nee_fix", "nee_blocks", "nee_records"])
 @pytest.mark.parametrize("shape", [(24, 40, 24), (33, 70, 29), (20, 512, 18), (17, 300, 21)])
 def test_poiseuille_nee_paths_bitwise(gpu, oracle, knob, nee_fix, shape):
     """The pipe along y with four cells per lane: its chunk waves collide the NEE-adjacent cells
-    (nee_chunks), and the NEE values come from k_nee_fix after the step launch (default), from
-    NEE blocks that re-pull and re-collide those cells (LBM_TUNE_NEE_FIX 1), or from NEE records
+    (nee_chunks), and the NEE values come from NEE blocks that re-pull and re-collide those cells
+    (LBM_TUNE_NEE_FIX 1, the default), from k_nee_fix after the step launch (3), or from NEE records
     (2, where every chunk holds at most 8 NEE-adjacent cells: rows of 300 and 512 cells; the 40-
     and 70-cell rows fall back to k_nee_fix).  All bit for bit against the oracle, populations
     included (the read-outs put the records' values into the NEE cells' slots), through the

@@ -11,12 +11,14 @@ PER_CELL = 1 + 1 + 4 + 4 + 16
 
 
 def test_pipe_device_bytes(gpu):
-    """C3's pipe (128 x 512 x 128, rows along y) takes k_nee_fix, whose (rho, u) records are one
+    """C3's pipe (128 x 512 x 128, rows along y) with k_nee_fix (LBM_TUNE_NEE_FIX 3), whose (rho, u) records are one
     16-B slot per NEE-adjacent cell (25.7 k cells), not one per box cell (8.4 M: 134 MB more,
     round 5).  The context holds its two population buffers plus 26 B per cell slot and small
     work lists; the placement probe's candidates are gone when lbm_create returns."""
     from lbm_amd import cases
-    lat, _ = cases.poiseuille(128, 512, 128)
+    import lbm_amd
+    with lbm_amd.tuned(lbm_amd.TUNE_NEE_FIX, 3):
+        lat, _ = cases.poiseuille(128, 512, 128)
     assert lat.nee_path()["path"] == "fix"
     st, sc = lat.storage(), lat.setup_cost()
     expect = st["bytes"] + PER_CELL * st["cells"]
@@ -46,8 +48,8 @@ def test_placement_peak_is_reported(gpu):
 def test_nee_fix_records_compact(gpu, knob, case):
     """k_nee_fix's records numbered by storage rank: the pipe's chunk list (one NEE-adjacent cell
     per chunk) and the upsampled bifurcation's compact 4-cell group list (64-entry slices, several
-    NEE-adjacent cells per wave) against the default of the other NEE path (NEE blocks,
-    LBM_TUNE_NEE_FIX 1), bit for bit -- which the oracle pins (test_poiseuille_nee_paths_bitwise,
+    NEE-adjacent cells per wave; LBM_TUNE_NEE_FIX 3) against the default NEE path (NEE blocks),
+    bit for bit -- which the oracle pins (test_poiseuille_nee_paths_bitwise,
     test_bifurcation_upsampled_bitwise)."""
     import numpy as np
     from lbm_amd import cases
@@ -65,8 +67,8 @@ def test_nee_fix_records_compact(gpu, knob, case):
         lat.close()
         return path, h, f, m
 
-    p0, h0, f0, m0 = run(0)
-    p1, h1, f1, m1 = run(1)
+    p0, h0, f0, m0 = run(3)
+    p1, h1, f1, m1 = run(0)
     assert (p0, p1) == ("fix", "blocks")
     assert np.array_equal(f0.view(np.uint32), f1.view(np.uint32))
     assert np.array_equal(m0.view(np.uint32), m1.view(np.uint32))
