@@ -217,9 +217,7 @@ typedef enum {
                                    ranges of several rounds of waves (vessel trees), one contiguous
                                    eighth of the chunks per XCD elsewhere; L = 1..16 runs of 2^(L-1) workgroups, XCD x taking
                                    runs x, x + 8, x + 16, ...; 17 one eighth per XCD everywhere */
-  LBM_TUNE_BLOCK_WAVES = 14,    /* workgroup size of the 4-cell chunk-list kernel (dense box, no NEE
-                                   records): 0 (default) and 4 four waves, 2 two waves */
-  LBM_TUNE_COUNT = 15
+  LBM_TUNE_COUNT = 14
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

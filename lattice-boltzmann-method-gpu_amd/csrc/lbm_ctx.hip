@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -99,7 +99,6 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   bool stride = false;    // grid-stride chunk loop (LBM_TUNE_GRID_STRIDE)
   double lane_fill = 1.0; // 4-cell path: mean share of chunk lanes with a cell to update
   bool quarter = false;   // one cell per lane (small ranges)
-  int wpb = 4;            // waves per workgroup of the chunk kernel (LBM_TUNE_BLOCK_WAVES)
 };
 }  // namespace
 
@@ -424,7 +423,6 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
-  a.wpb = r.wpb;
   // LBM_TUNE_XCD_RUN 0 (auto): round robin (runs of one block) for the 4-cell chunk lists whose
   // rows run along y -- the pipe, C3: 184 -> 176 us per step in rocprof, where LDC 256^3 and
   // 512^3 run 9% / 4% slower that way (profiles/r05p_c3_posts_xcd_rocprof.log,
@@ -918,17 +916,6 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     RCK(upload(c, &r.nee_mac_base, base));
     RCK(upload(c, &r.cell_mac, cm));
   }
-  // two-wave workgroups for dense chunk lists (LBM_TUNE_BLOCK_WAVES 2, A/B): the chunk blocks and
-  // the NEE blocks take two waves each
-  if (g_tune[LBM_TUNE_BLOCK_WAVES] == 2 && !r.quarter && !r.groups && !r.stride && !r.nee_records && !cv &&
-      r.nchunks > 0) {
-    r.wpb = 2;
-    r.main_blocks = std::max(8, ((r.nchunks + 1) / 2 + 7) / 8 * 8);
-    if (!r.nee_fix && r.n_nee > 0) {
-      r.nee_waves = std::min(r.nee_waves, 2);
-      r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);
-    }
-  }
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
 }
@@ -1328,10 +1315,9 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17, 4};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
-      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3)) ||
-      (knob == LBM_TUNE_BLOCK_WAVES && (value == 1 || value == 3))) {
+      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
     return LBM_ERR_ARG;
   }

@@ -1435,12 +1435,6 @@ template <bool FAST, bool SW, bool MASK, bool STRIDE = false, bool GROUPS = fals
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(const MainArgs a) {
   step_body<FAST, false, SW, MASK, STRIDE, GROUPS, COMPACT, BOX, kBlock / 64, REC>(a);
 }
-// the same with two-wave workgroups (LBM_TUNE_BLOCK_WAVES 2; dense chunk lists without records):
-// a workgroup's slots free when its slowest wave ends, so smaller workgroups waste fewer of them
-template <bool FAST, bool SW, bool MASK, bool BOX = false>
-__global__ __launch_bounds__(kBlockW2) __attribute__((amdgpu_waves_per_eu(2))) void k_step_w2(const MainArgs a) {
-  step_body<FAST, false, SW, MASK, false, false, false, BOX, kBlockW2 / 64>(a);
-}
 // one cell per lane (small lattices, latency-bound): registers capped for four waves per SIMD
 template <bool SW, bool GROUPS = false, bool STRIDE = false, bool COMPACT = false, bool BOX = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_step1(const MainArgs a) {
@@ -2183,18 +2177,6 @@ hipError_t launch_step(const MainArgs& a, hipStream_t s) {
     else k = sw ? k_step<false, true, false> : k_step<false, false, false>;
   }
   const bool c1 = !(a.box && !a.swap && !a.groups && !a.chunk_stride) && a.rowrec && a.quarter;
-  if (a.wpb == 2) {  // two-wave workgroups: dense chunk lists only (lbm_ctx's build_range)
-    if (a.quarter || a.groups || a.rowrec || a.chunk_stride || a.nee_rec_base) return hipErrorInvalidValue;
-    const bool bx = a.box && !a.swap;
-    if (a.fast_div) k = bx ? (a.lane_masks ? k_step_w2<true, false, true, true> : k_step_w2<true, false, false, true>)
-                        : sw ? (a.lane_masks ? k_step_w2<true, true, true> : k_step_w2<true, true, false>)
-                             : (a.lane_masks ? k_step_w2<true, false, true> : k_step_w2<true, false, false>);
-    else k = bx ? (a.lane_masks ? k_step_w2<false, false, true, true> : k_step_w2<false, false, false, true>)
-                : sw ? (a.lane_masks ? k_step_w2<false, true, true> : k_step_w2<false, true, false>)
-                     : (a.lane_masks ? k_step_w2<false, false, true> : k_step_w2<false, false, false>);
-    hipLaunchKernelGGL(k, grid, dim3(kBlockW2), lds, s, a);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(k, grid, dim3(c1 ? kBlock1c : kBlock), lds, s, a);
   return hipGetLastError();
 }

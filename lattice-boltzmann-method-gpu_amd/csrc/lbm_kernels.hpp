@@ -16,7 +16,6 @@ namespace lbm {
 constexpr int kChunk = 256;
 constexpr int kQ = 19;
 constexpr int kBlock = 256;  // 4 wavefronts, one chunk each
-constexpr int kBlockW2 = 128;  // LBM_TUNE_BLOCK_WAVES 2: two-wave workgroups of the dense 4-cell chunk path
 // the one-cell kernel over compact rows (vessel trees): 2 wavefronts per workgroup, so that a
 // few thousand waves spread evenly over the CUs (interleaved A/B: C4 8.74 -> 8.46 us, coronary
 // 37.5 -> 36.0 us; one-wave workgroups halve its residency, profiles/r04_workgroup_size_ab.log)
@@ -171,7 +170,6 @@ struct MainArgs {
   // red_partial[0 .. red_n) -- the partials of the previous step's launch, complete at this
   // launch's start -- and runs the residual logic, so a step is one launch, not two.
   int red_blocks;
-  int wpb;              // waves per workgroup of the 4-cell chunk kernels: 4 (kBlock), or 2 (kBlockW2)
   int red_last;         // 1: the reduction group trails the grid instead of leading it
   const double* red_partial;
   int red_n;
