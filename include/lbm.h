@@ -403,6 +403,11 @@ int lbm_comm_info(lbm_ctx* ctx, int* rank, int* nranks);
  * synchronising lbm_step, a read-out) sees a failed peer, which exercises the abort path above.
  * Only contexts with an RCCL communicator wait that way (LBM_ERR_STATE otherwise). */
 int lbm_debug_fail_next_wait(lbm_ctx* ctx);
+/* Test hook (not a reference interface): a quiet NaN into all 19 slots of every wall cell of both
+ * population buffers.  Where bounce-back is on the consumer side no step after the first reads a
+ * wall slot, so the fields go on bit for bit; where it is on the producer side the next step
+ * pulls the NaNs. */
+int lbm_debug_poison_walls(lbm_ctx* ctx);
 
 /* Single-device loopback decomposition (test and debug path): n contexts, each a z-slab of
  * one lattice on the same device, stepped together with device-to-device halo copies. */

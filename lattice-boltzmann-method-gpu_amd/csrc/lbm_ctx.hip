@@ -2670,6 +2670,17 @@ int lbm_comm_info(lbm_ctx* c, int* rank, int* nranks) {
   return LBM_OK;
 }
 
+int lbm_debug_poison_walls(lbm_ctx* c) {
+  if (!c) return LBM_ERR_ARG;
+  RCK(lbm_sync(c));
+  const int64_t n = c->compact ? c->ncell_c : c->L.ncell;
+  const uint8_t* t = c->compact ? c->ctype : c->type;
+  for (int b = 0; b < 2; ++b) HIPCK(c, launch_poison_walls(c->buf[b], t, n, c->s_comp));
+  HIPCK(c, hipStreamSynchronize(c->s_comp));
+  c->macros_stale = true;
+  return LBM_OK;
+}
+
 int lbm_debug_fail_next_wait(lbm_ctx* c) {
   if (!c) return LBM_ERR_ARG;
   if (!c->comm) {

@@ -2074,6 +2074,14 @@ __global__ void k_pop_scatter(float* __restrict__ dd, const float* __restrict__ 
     if (d >= 0) dd[aidx(d, q)] = sc[aidx(cell, q)];
   }
 }
+// test hook (lbm_debug_poison_walls): a quiet NaN into all 19 slots of every wall cell of f
+__global__ void k_poison_walls(float* __restrict__ f, const uint8_t* __restrict__ type, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * kQ; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cell = i / kQ;
+    const int q = (int)(i - cell * kQ);
+    if ((type[cell] & kClassMask) == kWall) f[aidx(cell, q)] = __builtin_nanf("");
+  }
+}
 template <class T>
 __global__ void k_cell_gather(T* __restrict__ dc, const T* __restrict__ sd, const int* __restrict__ cmap, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2508,6 +2516,10 @@ hipError_t launch_pop_compact(float* dst, const float* src, const int* cmap, int
   const dim3 g(grid_for(n * kQ, 256));
   if (to_compact) hipLaunchKernelGGL(k_pop_gather, g, dim3(256), 0, s, dst, src, cmap, n);
   else hipLaunchKernelGGL(k_pop_scatter, g, dim3(256), 0, s, dst, src, cmap, n);
+  return hipGetLastError();
+}
+hipError_t launch_poison_walls(float* f, const uint8_t* type, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_poison_walls, dim3(grid_for(n * kQ, 256)), dim3(256), 0, s, f, type, n);
   return hipGetLastError();
 }
 hipError_t launch_cell_gather(void* dst, const void* src, const int* cmap, int64_t n, int elem_bytes, hipStream_t s) {

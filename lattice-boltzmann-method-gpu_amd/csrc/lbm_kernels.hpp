@@ -289,6 +289,8 @@ hipError_t launch_probe_fill(void* dst, int64_t n4, hipStream_t s);
 hipError_t launch_pop_compact(float* dst, const float* src, const int* cmap, int64_t n, int to_compact,
                               hipStream_t s);
 hipError_t launch_cell_gather(void* dst, const void* src, const int* cmap, int64_t n, int elem_bytes, hipStream_t s);
+// test hook: NaN into every slot of the wall cells (class kWall) of population buffer f, n cells
+hipError_t launch_poison_walls(float* f, const uint8_t* type, int64_t n, hipStream_t s);
 
 // halo: pack populations qs[0..nq) of storage plane zs into buf[nq][plane] / unpack
 hipError_t launch_pack(const float* f, float* buf, int zs, int64_t plane, const int* qs_dev, int nq,

@@ -89,7 +89,8 @@ LBM_SYMBOLS = [
     "lbm_get_geo", "lbm_get_counts", "lbm_profile", "lbm_stats", "lbm_kernel_times", "lbm_get_boundary_cells", "lbm_get_storage", "lbm_get_numerics",
     "lbm_get_nee_path", "lbm_get_setup_cost",
     "lbm_get_layout", "lbm_get_launch_shape", "lbm_buffer_placement", "lbm_checkpoint_save", "lbm_checkpoint_load",
-    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_debug_fail_next_wait", "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
+    "lbm_rccl_unique_id", "lbm_attach_rccl", "lbm_comm_info", "lbm_debug_fail_next_wait", "lbm_debug_poison_walls",
+    "lbm_group_step", "lbm_probe_stream", "lbm_probe_stream_shapes",
 ]
 HOST_SYMBOLS = [
     "lbmh_geo_ldc", "lbmh_geo_poiseuille", "lbmh_geo_mask", "lbmh_read_geo_txt", "lbmh_read_bc_txt",
@@ -196,6 +197,7 @@ def lbm_lib() -> C.CDLL:
             "lbm_attach_rccl": (C.c_int, [P, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
             "lbm_comm_info": (C.c_int, [P, ip, ip]),
             "lbm_debug_fail_next_wait": (C.c_int, [P]),
+            "lbm_debug_poison_walls": (C.c_int, [P]),
             "lbm_group_step": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, f32p]),
             "lbm_probe_stream": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p]),
             "lbm_probe_stream_shapes": (C.c_int, [C.c_int, C.c_int64, C.c_int, f64p, C.c_int, ip]),
@@ -639,6 +641,10 @@ class Lattice:
     def debug_fail_next_wait(self):
         """Test hook: this context's next wait sees a failed RCCL peer (lbm_debug_fail_next_wait)."""
         self._ck(lbm_lib().lbm_debug_fail_next_wait(self.h), "lbm_debug_fail_next_wait")
+
+    def debug_poison_walls(self):
+        """Test hook: NaN into every wall cell's slots of both population buffers (lbm_debug_poison_walls)."""
+        self._ck(lbm_lib().lbm_debug_poison_walls(self.h), "lbm_debug_poison_walls")
 
     def attach_rccl(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

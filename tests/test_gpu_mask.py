@@ -417,3 +417,52 @@ def test_consumer_side_steps_write_no_wall_slot(gpu, knob, path):
     bad = np.count_nonzero(got.view(np.uint32) != sentinel.view(np.uint32))
     assert bad == 0, f"{path}: {bad} wall slots written"
     lat.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["bif_1cell_compact", "bif_4cell_compact", "coronary_1cell_compact", "ldc_1cell_box",
+                                  "pipe_producer"])
+def test_consumer_side_steps_read_no_wall_slot(gpu, knob, path):
+    """The property the no-write check above stands in for, tested directly: with bounce-back on
+    the consumer side no step after the first reads a wall slot.  Two identical lattices step
+    once; then every slot of every wall cell of both buffers of one of them becomes a quiet NaN
+    (lbm_debug_poison_walls: the wall slots whole 16-B stores cover included) and both step on --
+    fields, populations of the fluid cells and residuals stay bit for bit equal.  A lattice that
+    bounces back on the producer side pulls the NaNs at once, which shows the poison reaches
+    every wall slot a step could read."""
+    from lbm_amd import cases
+    import lbm_amd
+    if path == "bif_4cell_compact":
+        knob(lbm_amd.TUNE_CELLS_PER_LANE, 4)
+        knob(lbm_amd.TUNE_GROUPS, 2)
+        knob(lbm_amd.TUNE_COMPACT, 2)
+
+    def make():
+        if path.startswith("bif"):
+            return cases.bifurcation(1)[0]
+        if path.startswith("coronary"):
+            raw, ends = cases.coronary_small_vessel()
+            return cases.coronary(raw, ends)[0]
+        if path == "ldc_1cell_box":
+            return cases.ldc_device(32, 32, 32)
+        return cases.poiseuille(20, 28, 20)[0]
+
+    a, b = make(), make()
+    if path != "pipe_producer":
+        assert a.launch_shape()["cells_per_lane"] == (4 if path == "bif_4cell_compact" else 1)
+    geo = a.geo()
+    fluid = geo == (3 if path.startswith("ldc") else 4)
+    a.step(1)
+    b.step(1)
+    b.debug_poison_walls()
+    ha, hb = a.step(25), b.step(25)
+    mb = np.stack(b.macros())[:, fluid]
+    if path == "pipe_producer":
+        assert not np.all(np.isfinite(mb)), "the poisoned wall slots never reached a fluid cell"
+        return
+    ma = np.stack(a.macros())[:, fluid]
+    assert np.array_equal(ma.view(np.uint32), mb.view(np.uint32)), f"{path}: fields differ after poisoning the walls"
+    assert np.array_equal(a.f()[:, fluid].view(np.uint32), b.f()[:, fluid].view(np.uint32))
+    assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32))
+    a.close()
+    b.close()
