@@ -573,7 +573,7 @@ def run(args, world, rank, local, n, nzg, cpu_proc):
             "frac_of_stream_probe": round(achieved / probe, 4) if probe else None,
             "stream_probe": "lbm_probe_stream: best of 11 streaming-copy shapes (16-B vectors, grid-stride, "
                             "per-XCD regions or k_step-like 16-KB wave tiles, plain or non-temporal, the tiles also by "
-                            "LDS-DMA; read + write bytes / time) between two of up to sixteen 8-GiB allocations, picked by "
+                            "LDS-DMA; read + write bytes / time) between two of up to twenty 8-GiB allocations, picked by "
                             "the population buffers' placement rule (write-sweep rank, then the quickest tile-copy "
                             "pair of the four fastest) on this GPU in this run",
             "stream_probe_shapes_gbs": probe_shapes,

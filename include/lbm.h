@@ -168,7 +168,7 @@ typedef enum {
   LBM_TUNE_EXACT_DIV = 2,       /* 1: the compiler's division by tau everywhere */
   LBM_TUNE_FUSED_RESIDUAL = 3,  /* 1 (default): the residual rides in the next step's launch */
   LBM_TUNE_BUFFER_ALLOC = 4,    /* population buffers: 0 (default) of the four fastest-writing of
-                                   up to sixteen allocations (lbm_buffer_placement), the pair whose
+                                   up to 64 allocations (lbm_buffer_placement), the pair whose
                                    tile copies both ways take the least time together; 1 the first
                                    two allocations; 2 the two fastest-writing (round 4) */
   LBM_TUNE_SYNC_TIMEOUT_S = 5,  /* RCCL contexts: a wait (lbm_sync, synchronising lbm_step, read-
@@ -325,12 +325,13 @@ int lbm_get_numerics(lbm_ctx* ctx, int* fast_div, int64_t* retried_chunks);
 /* Placement of the two population buffers (not a reference interface).  HBM write bandwidth
  * differs between allocations (~5.5 vs ~6.4 TB/s for 10-GB buffers on MI355X, stable per
  * allocation); when a buffer is larger than 256 MB (the MALL) and the device has room,
- * lbm_create allocates up to sixteen candidates, times one full-buffer write sweep of each and,
- * of the four fastest, keeps the pair whose tile copies both ways take the least time together
+ * lbm_create allocates up to 64 candidates, times one full-buffer write sweep of each and, of the
+ * four fastest, keeps the pair whose tile copies both ways take the least time together
  * (LBM_TUNE_BUFFER_ALLOC).  The candidates are held together for the duration of the probe:
  * lbm_create may TRANSIENTLY allocate up to 160 GiB of device memory (sixteen 10.2-GB
- * candidates at 512^3), never more than three quarters of the memory free when it starts; the
- * rest is freed before it returns (lbm_get_setup_cost reports the low point).  gbs[0..cap) receives the
+ * candidates at 512^3, 64 of 1.28 GB at 256^3), never more than three quarters of the memory
+ * free when it starts; the rest is freed before it returns (lbm_get_setup_cost reports the low
+ * point).  gbs[0..cap) receives the
  * candidates' rates (GB/s) in allocation order, *n their count (0: buffers of at most 256 MB,
  * or compact rows, not probed), chosen[2] the indices kept.  Nullable outputs. */
 int lbm_buffer_placement(lbm_ctx* ctx, double* gbs, int cap, int* n, int* chosen);
@@ -375,7 +376,7 @@ int lbm_get_storage(lbm_ctx* ctx, int* compact, int64_t* cells, int64_t* bytes);
  * one wave per 16-KB tile with all 16 loads per lane in flight, and that tile by LDS-DMA), `reps` timed
  * launches each (HIP events, after one untimed launch); *gbs = the best (read + write bytes) /
  * duration in GB/s.  The two buffers are picked as the population buffers are
- * (lbm_buffer_placement): of up to sixteen allocations of `bytes`, the pair among the four
+ * (lbm_buffer_placement): of up to 64 allocations of `bytes`, the pair among the four
  * fastest-writing whose tile copies both ways take the least time together. */
 int lbm_probe_stream(int device, int64_t bytes, int reps, double* gbs);
 /* The same, per copy shape: gbs_shape[i] = the best rate of shape i for i < min(cap, n);

@@ -1114,7 +1114,11 @@ hipError_t rank_pair(const std::vector<void*>& p, size_t bytes, hipStream_t st, 
 constexpr size_t kPlacementMinBytes = (size_t)256 << 20;
 constexpr size_t kPlacementBudget = (size_t)160 << 30;
 hipError_t buffer_placement(lbm_ctx* c, size_t bytes, size_t others) {
-  constexpr int kMaxCand = 16;
+  // up to 64 candidates (round 6): on a box whose sixteen 1.28-GB candidates all wrote at <= 5.5 TB/s
+  // (LDC 256^3 457-462 us per step), 48 found 5.8-6.1 TB/s pairs (422-426 us) in five rounds of
+  // fresh processes; 128 were no better than 64 (profiles/r06k_placement48_ab.log,
+  // r06l_placement64_vs128_ab.log)
+  constexpr int kMaxCand = 64;
   int ncand = 2;
   const bool probe = bytes > kPlacementMinBytes;
   if (g_tune[LBM_TUNE_BUFFER_ALLOC] != 1 && probe) {
@@ -2588,16 +2592,17 @@ int lbm_probe_stream_shapes(int device, int64_t bytes, int reps, double* gbs_sha
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
   // the same placement rule as the population buffers (buffer_placement, rank_pair): up to
-  // sixteen candidates within the same budget, ranked by a write sweep each, and of the four
-  // fastest the pair whose tile copies both ways take the least time together
+  // 64 candidates within the same budget (twenty 8-GiB ones), ranked by a write sweep each, and
+  // of the four fastest the pair whose tile copies both ways take the least time together
   {
     std::vector<void*> cand;
     std::vector<double> rate;
     size_t fr = 0, tot = 0;
     if (e == hipSuccess) e = hipMemGetInfo(&fr, &tot);
     const size_t sz = (size_t)n4 * 16;
+    const size_t budget = std::min(kPlacementBudget, fr / 4 * 3);
     const int ncand = (int)std::max<size_t>(
-        2, std::min<size_t>(std::min<size_t>(16, kPlacementBudget / sz), fr > sz ? (fr - sz) / sz : 0));
+        2, std::min<size_t>(std::min<size_t>(64, budget / sz), fr > sz ? (fr - sz) / sz : 0));
     for (int i = 0; i < ncand && e == hipSuccess; ++i) {
       void* q = nullptr;
       e = hipMalloc(&q, sz);

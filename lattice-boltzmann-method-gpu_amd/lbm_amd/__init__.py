@@ -611,9 +611,9 @@ class Lattice:
     def placement(self):
         """Population-buffer placement (lbm_buffer_placement): candidates' write rates (GB/s) and
         the two kept; an empty list when the first two allocations were taken unprobed."""
-        gbs, n, ch = (C.c_double * 16)(), C.c_int(), (C.c_int * 2)()
-        self._ck(lbm_lib().lbm_buffer_placement(self.h, gbs, 16, C.byref(n), ch), "lbm_buffer_placement")
-        return {"candidate_write_gbs": [round(gbs[i], 1) for i in range(min(n.value, 16))], "chosen": [ch[0], ch[1]]}
+        gbs, n, ch = (C.c_double * 256)(), C.c_int(), (C.c_int * 2)()
+        self._ck(lbm_lib().lbm_buffer_placement(self.h, gbs, 256, C.byref(n), ch), "lbm_buffer_placement")
+        return {"candidate_write_gbs": [round(gbs[i], 1) for i in range(min(n.value, 256))], "chosen": [ch[0], ch[1]]}
 
     def profile(self, enabled=True):
         """lbm_profile: True / 1 per-launch HIP events, 2 one event pair per lbm_step call

@@ -30,14 +30,14 @@ def test_pipe_device_bytes(gpu):
 
 
 def test_placement_peak_is_reported(gpu):
-    """LDC 256^3 (1.28-GB buffers, over the 256-MB threshold): lbm_create holds up to sixteen
+    """LDC 256^3 (1.28-GB buffers, over the 256-MB threshold): lbm_create holds up to 64
     placement candidates at once; the peak it reports covers them, and the memory it keeps is
     the two chosen buffers plus the per-cell arrays."""
     from lbm_amd import cases
     lat = cases.ldc_device(256, 256, 256)
     st, sc, pl = lat.storage(), lat.setup_cost(), lat.placement()
     n = len(pl["candidate_write_gbs"])
-    assert 2 <= n <= 16
+    assert 2 <= n <= 64
     one = st["bytes"] // 2
     assert sc["peak_bytes"] >= n * one * 0.99, (sc, n, one)
     assert sc["device_bytes"] <= st["bytes"] + PER_CELL * st["cells"] + (64 << 20), sc
