@@ -217,7 +217,12 @@ typedef enum {
                                    ranges of several rounds of waves (vessel trees), one contiguous
                                    eighth of the chunks per XCD elsewhere; L = 1..16 runs of 2^(L-1) workgroups, XCD x taking
                                    runs x, x + 8, x + 16, ...; 17 one eighth per XCD everywhere */
-  LBM_TUNE_COUNT = 14
+  LBM_TUNE_NEE_ORDER = 14,      /* dispatch order of the NEE blocks in the step launch: 0 (default) after
+                                   the chunk blocks for grid-stride group lists, before them elsewhere;
+                                   1 before; 2 after.  Results are bit-identical (the partial slots
+                                   keep their order) */
+  LBM_TUNE_NEE_WAVES = 15,      /* LAB */
+  LBM_TUNE_COUNT = 16
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);
 

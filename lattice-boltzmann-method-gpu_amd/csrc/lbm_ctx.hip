@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -68,6 +68,7 @@ struct Range {            // one launch: cells [c_lo, c_hi) u [c_lo2, c_hi2) wit
   // step launch, from those records and the cells' own post-collision slots (cells, cell_nl and
   // nee_bc are its list)
   bool nee_fix = false;
+  bool nee_last = false;  // NEE blocks dispatched after the chunk blocks (MainArgs::nee_last)
   int* nee_mac_base = nullptr;  // nee_fix: per work unit (chunk-list entry, 64-entry group-list slice), the
                                 // nee_mac slot of its first NEE-adjacent cell (MainArgs::nee_mac_base)
   int* cell_mac = nullptr;      // nee_fix: per NEE-list entry, its nee_mac slot
@@ -448,6 +449,7 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.stopped = c->conv_enabled ? &c->conv->stopped : nullptr;
   a.cells = r.cells; a.cell_nl = r.cell_nl; a.nee_bc = r.nee_bc; a.n_nee = r.n_nee;
   a.nee_blocks = r.nee_blocks; a.nee_waves = r.nee_waves;
+  a.nee_last = r.nee_last ? 1 : 0;
   a.nee_chunks = r.nee_chunks ? 1 : 0;
   a.nee_mac = r.nee_fix ? c->nee_mac : nullptr;
   a.nee_mac_base = r.nee_mac_base;
@@ -835,7 +837,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     const int64_t waves = (int64_t)r.main_blocks * ((cv ? kBlock1c : kBlock) / 64);  // four per SIMD fit
     r.one_round = waves <= (int64_t)cus * 16;
   }
-  r.nee_waves = nee_waves_for(r.n_nee, contig);
+  r.nee_waves = g_tune[LBM_TUNE_NEE_WAVES] ? g_tune[LBM_TUNE_NEE_WAVES] : nee_waves_for(r.n_nee, contig);
   r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);
   // the single-domain range of a lattice whose chunk waves collide the NEE-adjacent cells: the NEE
   // values from NEE blocks in the step launch that pull and collide every such cell again
@@ -915,6 +917,15 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     for (size_t i = 0; i < nee_list.size(); ++i) cm[i] = slot_of(nee_list[i]);
     RCK(upload(c, &r.nee_mac_base, base));
     RCK(upload(c, &r.cell_mac, cm));
+  }
+  // Where the NEE blocks go in the grid (LBM_TUNE_NEE_ORDER).  Grid-stride group lists (C4 x4):
+  // after the chunk blocks -- each loop wave's share of the list is fixed, so NEE blocks dispatched
+  // first made the loop's first workgroups start, and end, late; trailing, they fill the slots the
+  // loop's uneven end leaves idle (125.2 vs 130.7 us per step).  Chunk lists (C3): first, where
+  // they fill the first generation's load phase (trailing: 184.6 vs 176.8; profiles/r06q_nee_order_waves_ab.log)
+  {
+    const int order = g_tune[LBM_TUNE_NEE_ORDER];
+    r.nee_last = r.nee_blocks > 0 && (order == 2 || (order == 0 && r.groups && r.stride));
   }
   r.npart = r.main_blocks + r.nee_blocks;
   return LBM_OK;
@@ -1319,7 +1330,7 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17, 2, 4};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
       (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";

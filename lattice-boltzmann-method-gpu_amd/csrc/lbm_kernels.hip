@@ -1347,7 +1347,10 @@ __device__ __forceinline__ void step_body(const MainArgs& a) {  // WPB: wavefron
   // the reduction group leads the grid, or trails it (red_last: a grid of one round of waves,
   // whose chunk waves then all start at once)
   const int nwork = a.nee_blocks + a.main_blocks;
-  const int bx = a.red_last ? ((int)blockIdx.x < nwork ? (int)blockIdx.x : -1) : (int)blockIdx.x - a.red_blocks;
+  const int bd = a.red_last ? ((int)blockIdx.x < nwork ? (int)blockIdx.x : -1) : (int)blockIdx.x - a.red_blocks;
+  // nee_last: the NEE blocks trail the chunk blocks in dispatch order; their logical places, and
+  // with them the partial slots and the residual's summation order, do not change
+  const int bx = (a.nee_last && bd >= 0) ? (bd < a.main_blocks ? bd + a.nee_blocks : bd - a.main_blocks) : bd;
   const int rb = a.red_last ? (int)blockIdx.x - nwork : (int)blockIdx.x;
   if (bx < 0) {  // reduction group: its first block finishes the previous step
     slot = rb;

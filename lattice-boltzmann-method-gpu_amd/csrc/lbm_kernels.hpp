@@ -170,6 +170,7 @@ struct MainArgs {
   // red_partial[0 .. red_n) -- the partials of the previous step's launch, complete at this
   // launch's start -- and runs the residual logic, so a step is one launch, not two.
   int red_blocks;
+  int nee_last;         // 1: the NEE blocks are dispatched after the chunk blocks (grid-stride group lists)
   int red_last;         // 1: the reduction group trails the grid instead of leading it
   const double* red_partial;
   int red_n;
