@@ -221,7 +221,8 @@ typedef enum {
                                    the chunk blocks for grid-stride group lists, before them elsewhere;
                                    1 before; 2 after.  Results are bit-identical (the partial slots
                                    keep their order) */
-  LBM_TUNE_NEE_WAVES = 15,      /* LAB */
+  LBM_TUNE_NEE_WAVES = 15,      /* active waves per NEE block: 0 (default) by the list (1 for short,
+                                   scattered lists, else 4), or 1, 2, 4 */
   LBM_TUNE_COUNT = 16
 } lbm_tune_knob;
 int lbm_tune(int knob, int value);

@@ -1332,7 +1332,7 @@ const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int lbm_tune(int knob, int value) {
   static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17, 2, 4};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
-      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
+      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3)) || (knob == LBM_TUNE_NEE_WAVES && value == 3)) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
     return LBM_ERR_ARG;
   }
