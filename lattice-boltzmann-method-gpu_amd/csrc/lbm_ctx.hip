@@ -35,7 +35,7 @@ using namespace lbm;
 namespace {
 std::string g_create_error;
 // process-wide tuning knobs (lbm_tune), read by lbm_create / the step path
-int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0, 0, 0};
+int g_tune[LBM_TUNE_COUNT] = {0, 0, 0, 1, 0, 0, 0, 0, 0, 16, 0, 0, 0, 0, 0};
 constexpr int kUpSet[5] = {5, 11, 13, 15, 16};    // e_z = +1: cross the top face
 constexpr int kDownSet[5] = {6, 12, 14, 17, 18};  // e_z = -1: cross the bottom face
 
@@ -424,17 +424,19 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   a.partial = part ? part : r.part;
   a.chunks = r.chunks; a.chunk0 = r.chunk0; a.nchunks = r.nchunks; a.main_blocks = r.main_blocks; a.quarter = r.quarter ? 1 : 0;
   a.chunk_stride = r.stride ? 1 : 0;
-  // LBM_TUNE_XCD_RUN 0 (auto): round robin (runs of one block) for the 4-cell chunk lists whose
-  // rows run along y -- the pipe, C3: 184 -> 176 us per step in rocprof, where LDC 256^3 and
-  // 512^3 run 9% / 4% slower that way (profiles/r05p_c3_posts_xcd_rocprof.log,
-  // r05_xcd_run_ab.log); runs of four blocks for compact one-cell ranges of several rounds of
+  // LBM_TUNE_XCD_RUN 0 (auto): runs of four blocks (L = 3) for the 4-cell chunk lists whose rows
+  // run along y -- the pipe, C3: round robin (runs of one) took it from 184 to 176 us per step in
+  // rocprof in round 5, where LDC 256^3 and 512^3 run 9% / 4% slower that way
+  // (profiles/r05p_c3_posts_xcd_rocprof.log, r05_xcd_run_ab.log); with the NEE blocks in the
+  // launch (round 6) runs of four beat runs of one by ~0.8 us, 170.4-171.0 vs 171.1-172.8
+  // (r06m_c3_xcd_runs_ab.log, r06o_c3_xcd_runs_ab.log); runs of four blocks for compact one-cell ranges of several rounds of
   // waves -- the coronary tree: 31.1 -> 29.8 us, where one-round C4 runs slower interleaved
   // (r05_c1_xcd_ab.log, r05z_coronary_xcd_ab.log); one contiguous eighth per XCD elsewhere; 17:
   // eighths everywhere.  Not for grid-stride ranges: their waves take work by XCD (b & 7) and
   // round (b >> 3) whatever the order, so a run length would only move their partial slots
   a.xcd_run = (c->xcd_run == 17 || r.stride)                 ? 0
               : c->xcd_run > 0                               ? c->xcd_run
-              : (c->L.swap && !r.quarter && !r.groups)       ? 1
+              : (c->L.swap && !r.quarter && !r.groups)       ? 3
               : (c->compact && r.quarter && !r.one_round)    ? 3
                                                              : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;
@@ -837,7 +839,7 @@ int build_range(lbm_ctx* c, Range& r, int64_t lo, int64_t hi, const std::vector<
     const int64_t waves = (int64_t)r.main_blocks * ((cv ? kBlock1c : kBlock) / 64);  // four per SIMD fit
     r.one_round = waves <= (int64_t)cus * 16;
   }
-  r.nee_waves = g_tune[LBM_TUNE_NEE_WAVES] ? g_tune[LBM_TUNE_NEE_WAVES] : nee_waves_for(r.n_nee, contig);
+  r.nee_waves = nee_waves_for(r.n_nee, contig);
   r.nee_blocks = nee_grid(r.n_nee, r.nee_waves);
   // the single-domain range of a lattice whose chunk waves collide the NEE-adjacent cells: the NEE
   // values from NEE blocks in the step launch that pull and collide every such cell again
@@ -1330,9 +1332,9 @@ const char* lbm_version(void) { return "lbm-mi355x 0.2 (gfx950, D3Q19 BGK, AoSoA
 const char* lbm_last_error(const lbm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 int lbm_tune(int knob, int value) {
-  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17, 2, 4};
+  static const int hi[LBM_TUNE_COUNT] = {2, 4, 1, 1, 2, 86400, 8, 0, 2, 64, 2, 1, 3, 17, 2};
   if (knob < 0 || knob >= LBM_TUNE_COUNT || value < 0 || value > hi[knob] ||
-      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3)) || (knob == LBM_TUNE_NEE_WAVES && value == 3)) {
+      (knob == LBM_TUNE_CELLS_PER_LANE && (value == 2 || value == 3))) {
     g_create_error = "lbm_tune: unknown knob or value out of range";
     return LBM_ERR_ARG;
   }

@@ -35,7 +35,7 @@ LBM_SUM_FP64, LBM_SUM_CUB_TREE = 0, 1  # lbm_set_residual_order
 # lbm_tune knobs (include/lbm.h lbm_tune_knob)
 (TUNE_ROW_AXIS, TUNE_CELLS_PER_LANE, TUNE_EXACT_DIV, TUNE_FUSED_RESIDUAL, TUNE_BUFFER_ALLOC,
  TUNE_SYNC_TIMEOUT_S, TUNE_GRID_STRIDE, TUNE_INJECT_RCCL_FAULT, TUNE_GROUPS, TUNE_GROUP_SEGMENT, TUNE_COMPACT,
- TUNE_BOX, TUNE_NEE_FIX, TUNE_XCD_RUN, TUNE_NEE_ORDER, TUNE_NEE_WAVES) = range(16)
+ TUNE_BOX, TUNE_NEE_FIX, TUNE_XCD_RUN, TUNE_NEE_ORDER) = range(15)
 
 # reference per-case constants
 LDC_TAU, LDC_C_U, LDC_CH = 0.55, 2.4705, 0.0000655737                   # ldc.cu:49,55

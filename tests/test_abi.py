@@ -99,7 +99,7 @@ def test_tune_knobs_validated(lbm):
                 lbm.TUNE_FUSED_RESIDUAL: 1, lbm.TUNE_BUFFER_ALLOC: 0, lbm.TUNE_SYNC_TIMEOUT_S: 0,
                 lbm.TUNE_GRID_STRIDE: 0, lbm.TUNE_INJECT_RCCL_FAULT: 0, lbm.TUNE_GROUPS: 0,
                 lbm.TUNE_GROUP_SEGMENT: 16, lbm.TUNE_COMPACT: 0, lbm.TUNE_BOX: 0, lbm.TUNE_NEE_FIX: 0,
-                lbm.TUNE_XCD_RUN: 0, lbm.TUNE_NEE_ORDER: 0, lbm.TUNE_NEE_WAVES: 0}
+                lbm.TUNE_XCD_RUN: 0, lbm.TUNE_NEE_ORDER: 0}
     for knob, dflt in defaults.items():
         assert lbm.tune(knob, dflt) == dflt
     with lbm.tuned(lbm.TUNE_CELLS_PER_LANE, 4):
@@ -110,7 +110,7 @@ def test_tune_knobs_validated(lbm):
                         (lbm.TUNE_GRID_STRIDE, 9), (lbm.TUNE_INJECT_RCCL_FAULT, 1), (lbm.TUNE_GROUPS, 3),
                         (lbm.TUNE_GROUP_SEGMENT, 65), (lbm.TUNE_COMPACT, 3), (lbm.TUNE_BOX, 2),
                         (lbm.TUNE_NEE_FIX, 4), (lbm.TUNE_XCD_RUN, 18), (lbm.TUNE_BUFFER_ALLOC, 3),
-                        (lbm.TUNE_NEE_ORDER, 3), (lbm.TUNE_NEE_WAVES, 3), (lbm.TUNE_NEE_WAVES, 5)):
+                        (lbm.TUNE_NEE_ORDER, 3)):
         with pytest.raises(lbm.LbmError, match="unknown knob or value"):
             lbm.tune(knob, value)
     for knob, dflt in defaults.items():  # a rejected call leaves every knob as it was
