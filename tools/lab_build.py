@@ -48,9 +48,9 @@ PATCHES = {
     # wave timestamps (s_memrealtime, 100 MHz): every 4-cell chunk wave of the dense chunk path
     # records its start and end into g_lab_ts (lbm_lab_ts_copy), values unchanged
     "wave_ts": [("lbm_kernels.hip",
-                 "      acc = process_chunk<FAST, SW, MASK, false, false, BOX>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base\n    }",
+                 "      acc = process_chunk<FAST, SW, MASK, false, false, BOX, REC>(a, chunk_of(a, idx) * kChunk, lane, lm, idx);  // uniform base\n    }",
                  "      const unsigned long long t_in = wall_clock64();\n"
-                 "      acc = process_chunk<FAST, SW, MASK, false, false, BOX>(a, chunk_of(a, idx) * kChunk, lane, lm);  // uniform base\n"
+                 "      acc = process_chunk<FAST, SW, MASK, false, false, BOX, REC>(a, chunk_of(a, idx) * kChunk, lane, lm, idx);  // uniform base\n"
                  "      if (lane == 0 && idx < (1 << 18)) {\n"
                  "        g_lab_ts[2 * idx] = t_in;\n"
                  "        g_lab_ts[2 * idx + 1] = wall_clock64();\n"
