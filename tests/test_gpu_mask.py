@@ -466,3 +466,28 @@ def test_consumer_side_steps_read_no_wall_slot(gpu, knob, path):
     assert np.array_equal(ha.view(np.uint32), hb.view(np.uint32))
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["bif_x4", "pipe"])
+def test_nee_order_bitwise(gpu, knob, case):
+    """LBM_TUNE_NEE_ORDER moves only where the NEE blocks are dispatched (trailing the grid-stride
+    group lists by default, leading the pipe's chunk list): both orders step bit for bit alike,
+    residual histories included -- the blocks keep their logical places and partial slots."""
+    from lbm_amd import cases
+    knob(gpu.TUNE_CELLS_PER_LANE, 4)
+
+    def run(order):
+        with gpu.tuned(gpu.TUNE_NEE_ORDER, order):
+            lat = cases.bifurcation_upsampled(4)[0] if case == "bif_x4" else cases.poiseuille(40, 300, 36)[0]
+        assert lat.nee_path()["path"] == "blocks"
+        h = lat.step(11)
+        f = lat.f()
+        lat.close()
+        return f, h
+
+    f0, h0 = run(0)
+    for order in (1, 2):
+        f, h = run(order)
+        assert np.array_equal(f.view(np.uint32), f0.view(np.uint32)), f"{case} nee order {order}"
+        assert np.array_equal(h.view(np.uint32), h0.view(np.uint32)), (order, h, h0)
