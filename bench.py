@@ -144,14 +144,13 @@ def ldc_line(n: int, steps: int, dev: int, name: str):
     return timed_mlups(cases.ldc_device(n, n, n, device=dev), {"mlups": n ** 3}, steps, name=name)
 
 
-def c2_line(dev: int, lattices: int = 3, steps: int = 1000):
-    """Config C2 (LDC 256^3, 1000 steps) on `lattices` fresh lattices in turn, each with its own
-    buffer placement: the 1.28-GB population buffers' HBM write rates differ from allocation to
-    allocation, and with them C2's step time.  The line is the median
-    lattice's, with every lattice's step time, wall time and kept buffers' write rates beside it."""
-    name = "ldc_256^3 (C2)"
-    runs = [timed_mlups(cases.ldc_device(256, 256, 256, device=dev), {"mlups": 256 ** 3}, steps, name=name)
-            for _ in range(lattices)]
+def fresh_line(name: str, make, cells: dict, steps: int, lattices: int = 3):
+    """One secondary line over `lattices` fresh lattices in turn (make() builds one), each with its
+    own buffers: step times differ from allocation to allocation (C2's 1.28-GB population buffers'
+    HBM write rates) and from process to process (C3's slow mode, section 3).
+    The line is the median lattice's, with every lattice's step time, wall time and kept buffers'
+    write rates beside it."""
+    runs = [timed_mlups(make(), cells, steps, name=name) for _ in range(lattices)]
     order = sorted(range(lattices), key=lambda i: runs[i]["roofline"]["step_us"])
     out = dict(runs[order[lattices // 2]])
     us = [runs[i]["roofline"]["step_us"] for i in order]
@@ -166,6 +165,12 @@ def c2_line(dev: int, lattices: int = 3, steps: int = 1000):
                          "setup": r["setup"]} for r in runs],
     }
     return out
+
+
+def c2_line(dev: int, lattices: int = 3, steps: int = 1000):
+    """Config C2 (LDC 256^3, 1000 steps) on three fresh lattices (fresh_line)."""
+    return fresh_line("ldc_256^3 (C2)", lambda: cases.ldc_device(256, 256, 256, device=dev), {"mlups": 256 ** 3},
+                      steps, lattices)
 
 
 def c5_one_gpu(dev: int, steps: int = 500):
@@ -242,10 +247,11 @@ def config_lines(dev: int):
     bifurcation mask) as secondary lines: MLUPS over box cells and over the reference's
     NLATTICE (stored cells, its metric for sparse cases)."""
     out = {}
-    lat, geo = cases.poiseuille(128, 512, 128, device=dev)
+    geo = cases.geo_poiseuille(128, 512, 128)
     nl, _ = lbm_amd.index_transform(geo)
     k = "poiseuille_128x512x128 (C3)"
-    out[k] = timed_mlups(lat, {"mlups_box": geo.size, "mlups_nlattice": nl}, 1000, name=k)
+    out[k] = fresh_line(k, lambda: cases.poiseuille(128, 512, 128, device=dev)[0],
+                        {"mlups_box": geo.size, "mlups_nlattice": nl}, 1000)
     # the same lattice on the x-row layout (lbm_desc.row_axis = 1), for comparison
     with lbm_amd.tuned(lbm_amd.TUNE_ROW_AXIS, 1):
         lat, geo = cases.poiseuille(128, 512, 128, device=dev)

@@ -18,7 +18,7 @@ for k, v in p.get("secondary", {}).items():
     print(f"  {k:48s} {m:>10} MLUPS  wall {v.get('ms_per_step')} ms  step {rl.get('step_us')} us  frac {rl.get('frac')}"
           f"  rocprof {ro.get('k_step_us')}/{ro.get('k_nee_fix_us')} frac {ro.get('frac_k_step')}  nee {v.get('nee_values')}")
     if "fresh_lattices" in v:
-        print("     C2 lattices", v["fresh_lattices"]["step_us_min_median_max"], v["fresh_lattices"]["frac_min_median_max"],
+        print("     fresh lattices", v["fresh_lattices"]["step_us_min_median_max"], v["fresh_lattices"]["frac_min_median_max"],
               [x["kept_write_gbs"] for x in v["fresh_lattices"]["per_lattice"]])
 cb = p.get("cpu_baseline")
 if cb:

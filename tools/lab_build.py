@@ -51,12 +51,14 @@ PATCHES = {
                  "      acc = process_chunk<FAST, SW, MASK, false, false, BOX, REC>(a, chunk_of(a, idx) * kChunk, lane, lm, idx);  // uniform base\n    }",
                  "      const unsigned long long t_in = wall_clock64();\n"
                  "      acc = process_chunk<FAST, SW, MASK, false, false, BOX, REC>(a, chunk_of(a, idx) * kChunk, lane, lm, idx);  // uniform base\n"
-                 "      if (lane == 0 && idx < (1 << 18)) {\n"
-                 "        g_lab_ts[2 * idx] = t_in;\n"
-                 "        g_lab_ts[2 * idx + 1] = wall_clock64();\n"
+                 "      if (lane == 0 && idx < (1 << 20)) {\n"
+                 "        unsigned xcc;\n"
+                 "        asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\" : \"=s\"(xcc));\n"
+                 "        g_lab_ts[2 * idx] = t_in | ((unsigned long long)(xcc & 15) << 56);\n"
+                 "        g_lab_ts[2 * idx + 1] = wall_clock64() | ((unsigned long long)x << 56);\n"
                  "      }\n    }"),
                 ("lbm_kernels.hip", "__device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {",
-                 "__device__ unsigned long long g_lab_ts[2 << 18];\n"
+                 "__device__ unsigned long long g_lab_ts[2 << 20];\n"
                  "__device__ void residual_logic(ConvState* cv, double S, float* hist_slot) {"),
                 ("lbm_kernels.hip", "}  // namespace lbm\n",
                  "}  // namespace lbm\n"
@@ -109,6 +111,11 @@ PATCHES = {
               ("lbm_kernels.hip", "  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, s, a);\n  return hipGetLastError();\n}\n\nhipError_t launch_reduce(",
                "  hipLaunchKernelGGL(k, grid, dim3(64), 0, s, a);\n  return hipGetLastError();\n}\n\nhipError_t launch_reduce(")],
     # the compact one-cell kernel in four-wave / one-wave workgroups
+    # k_step1c (compact rows, one cell per lane) capped for five / six waves per SIMD
+    "c1_w5": [("lbm_kernels.hip", "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(4))) void k_step1c(",
+               "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(5))) void k_step1c(")],
+    "c1_w6": [("lbm_kernels.hip", "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(4))) void k_step1c(",
+               "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(6))) void k_step1c(")],
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
     "c1_wg64": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 64;")],
     # placement over up to 160 GiB of candidates (15 at 512^3 instead of 6)

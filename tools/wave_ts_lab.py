@@ -37,12 +37,17 @@ def summarise(w):
     lat.sync()
     lat.step(1, history=False)
     lat.sync()
-    n = min(n, 1 << 18)
+    n = min(n, 1 << 20)
     buf = (C.c_ulonglong * (2 * n))()
     rc = lbm_amd.lbm_lib().lbm_lab_ts_copy(buf, 2 * n)
     assert rc == 0, rc
     lat.close()
-    ts = np.frombuffer(buf, dtype=np.uint64).reshape(n, 2).astype(np.int64)
+    ts = np.frombuffer(buf, dtype=np.uint64).reshape(n, 2).copy()
+    grp = (ts[:, 1] >> np.uint64(56)).astype(np.int64)  # the block's XCD group (dispatch index mod 8)
+    xcc = (ts[:, 0] >> np.uint64(56)).astype(np.int64)  # HW_REG_XCC_ID of the wave's XCD
+    ts[:, 0] &= np.uint64((1 << 56) - 1)
+    ts[:, 1] &= np.uint64((1 << 56) - 1)
+    ts = ts.astype(np.int64)
     t0 = ts[:, 0].min()
     s = (ts[:, 0] - t0) / 100.0  # us (100 MHz)
     e = (ts[:, 1] - t0) / 100.0
@@ -61,7 +66,14 @@ def summarise(w):
             "lifetime_by_decile_of_start_us": [round(float(life[(s >= np.percentile(s, 10 * k)) &
                                                               (s <= np.percentile(s, 10 * k + 10))].mean()), 2)
                                                for k in range(10)],
-            "occupancy_every_2us": occ}
+            "occupancy_every_2us": occ,
+            "by_xcd_group": [{"waves": int((grp == g).sum()), "first_start_us": round(float(s[grp == g].min()), 2),
+                              "last_start_us": round(float(s[grp == g].max()), 2),
+                              "last_end_us": round(float(e[grp == g].max()), 2),
+                              "p99_end_us": round(float(np.percentile(e[grp == g], 99)), 2),
+                              "mean_life_us": round(float(life[grp == g].mean()), 2),
+                              "xcc": sorted(set(int(v) for v in xcc[grp == g]))}
+                             for g in range(8) if (grp == g).any()]}
 
 
 for w in sys.argv[1:]:
