@@ -116,6 +116,23 @@ PATCHES = {
                "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(5))) void k_step1c(")],
     "c1_w6": [("lbm_kernels.hip", "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(4))) void k_step1c(",
                "__global__ __launch_bounds__(kBlock1c) __attribute__((amdgpu_waves_per_eu(6))) void k_step1c(")],
+    # the population buffers' and per-cell arrays' device addresses (lbm_lab_ptrs; tools/c3_modes_lab.py)
+    "ptrs": [("lbm_ctx.hip", "int lbm_buffer_placement(lbm_ctx* c, double* gbs, int cap, int* n, int* chosen) {",
+              "extern \"C\" int lbm_lab_ptrs(lbm_ctx* c, unsigned long long* out) {\n"
+              "  out[0] = (unsigned long long)c->alloc[0];\n  out[1] = (unsigned long long)c->alloc[1];\n"
+              "  out[2] = (unsigned long long)c->type;\n  out[3] = (unsigned long long)c->whole.chunks;\n"
+              "  out[4] = (unsigned long long)c->whole.cells;\n  out[5] = (unsigned long long)c->cur;\n  return 0;\n}\n"
+              "int lbm_buffer_placement(lbm_ctx* c, double* gbs, int cap, int* n, int* chosen) {")],
+    # the kept pair of population buffers at least four buffer sizes apart in the address space
+    # when the top writers allow it (C3's slow mode came with neighbouring buffers, r06zi)
+    "pair_far": [("lbm_ctx.hip", "    float best = 0.f;\n    for (int i = 0; i < K; ++i)",
+                  "    float best = 0.f;\n"
+                  "    auto pen = [&](int i, int j) {\n"
+                  "      const int64_t d = (int64_t)((const char*)p[order[i]] - (const char*)p[order[j]]);\n"
+                  "      return (d < 0 ? -d : d) >= 4 * (int64_t)bytes ? 0.f : 1e6f;\n    };\n"
+                  "    for (int i = 0; i < K; ++i)"),
+                 ("lbm_ctx.hip", "        if (best == 0.f || t[i][j] + t[j][i] < best) {\n          best = t[i][j] + t[j][i];",
+                  "        if (best == 0.f || t[i][j] + t[j][i] + pen(i, j) < best) {\n          best = t[i][j] + t[j][i] + pen(i, j);")],
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
     "c1_wg64": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 64;")],
     # placement over up to 160 GiB of candidates (15 at 512^3 instead of 6)
