@@ -133,6 +133,16 @@ PATCHES = {
                   "    for (int i = 0; i < K; ++i)"),
                  ("lbm_ctx.hip", "        if (best == 0.f || t[i][j] + t[j][i] < best) {\n          best = t[i][j] + t[j][i];",
                   "        if (best == 0.f || t[i][j] + t[j][i] + pen(i, j) < best) {\n          best = t[i][j] + t[j][i] + pen(i, j);")],
+    # the pipe's pull-phase priority (product: 2, lbm_kernels.hip kPrio) at 3 / 1, or also raised
+    # for the store phase
+    "prio3": [("lbm_kernels.hip", "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);",
+               "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(3);")],
+    "prio1": [("lbm_kernels.hip", "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);",
+               "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);")],
+    "prio_st": [("lbm_kernels.hip", "  float* d = a.dst + aidx(c, 0);\n  if (whole) {",
+                 "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);\n  float* d = a.dst + aidx(c, 0);\n  if (whole) {")],
+    # the pull-phase priority for the cavity's x-row chunk waves too
+    "prio_all": [("lbm_kernels.hip", "  constexpr bool kPrio = SW && !GROUPS;", "  constexpr bool kPrio = !GROUPS;")],
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
     "c1_wg64": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 64;")],
     # placement over up to 160 GiB of candidates (15 at 512^3 instead of 6)
