@@ -703,11 +703,12 @@ __device__ __forceinline__ double process_chunk(const MainArgs& a, int64_t cb, i
   // COMPACT: bounce-back on the consumer side (bb_own_*); step 0 of a case whose walls do not
   // bounce back yet pulls the walls raw
   const bool consumer = COMPACT && a.bb_pull && !a.bb_raw;
-  // y-row chunk lists (the pipe): the wave issues its pulls and its stores at raised priority and
-  // drops it for the arithmetic, so that a SIMD's other wave, in its arithmetic, does not hold back
-  // the memory instructions (C3 170.5 vs 171.8 us per step for the pulls, r06zl, and 169.9 vs 170.5
-  // with the stores, r06zm; the cavity's x rows run 1.3% slower that way at 256^3, r06zk)
-  constexpr bool kPrio = SW && !GROUPS;
+  // y rows (the pipe's chunk lists, the upsampled bifurcation's group lists): the wave issues its
+  // pulls and its stores at raised priority and drops it for the arithmetic, so that a SIMD's
+  // other wave, in its arithmetic, does not hold back the memory instructions (C3 170.5 vs 171.8
+  // us per step for the pulls, r06zl, and 169.9 vs 170.5 with the stores, r06zm; C4 x4 123.6 vs
+  // 124.5, r06zq; the cavity's x rows run 1.3% slower that way at 256^3, r06zk)
+  constexpr bool kPrio = SW;
   if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);
   if constexpr (GROUPS) {
     // compact groups: lane = one 4-cell group of the range's list (cb: the wave's first entry);

@@ -141,6 +141,16 @@ PATCHES = {
                "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);")],
     "prio_st": [("lbm_kernels.hip", "  float* d = a.dst + aidx(c, 0);\n  if (whole) {",
                  "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);\n  float* d = a.dst + aidx(c, 0);\n  if (whole) {")],
+    # one-cell waves: pulls and stores at raised priority, the arithmetic at 0 (compact rows only
+    # raise it at the start; collide_cell1's flips are no-ops elsewhere until the stores)
+    "c1_prio": [("lbm_kernels.hip", "  const int64_t c = (a.c_lo & ~int64_t(63)) + w * 64 + lane;\n",
+                 "  const int64_t c = (a.c_lo & ~int64_t(63)) + w * 64 + lane;\n  __builtin_amdgcn_s_setprio(2);\n"),
+                ("lbm_kernels.hip", "  float rho = 0.f;\n#pragma unroll\n  for (int q = 0; q < kQ; ++q) rho = rho + f[q];\n  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;\n  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;\n  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;\n  if (__any(nee) && a.tau_fast",
+                 "  __builtin_amdgcn_s_setprio(0);\n  float rho = 0.f;\n#pragma unroll\n  for (int q = 0; q < kQ; ++q) rho = rho + f[q];\n  const float ux = (f[1] - f[2] + f[7] + f[8] - f[9] - f[10] + f[11] + f[12] - f[13] - f[14]) / rho;\n  const float uy = (f[3] - f[4] + f[7] - f[8] + f[9] - f[10] + f[15] - f[16] + f[17] - f[18]) / rho;\n  const float uz = (f[5] - f[6] + f[11] - f[12] + f[13] - f[14] + f[15] + f[16] - f[17] - f[18]) / rho;\n  if (__any(nee) && a.tau_fast"),
+                ("lbm_kernels.hip", "  fix_store_all<SW>(f, a.dst, c, ad, (t & kWallAdj) ? links : 0u, AllQ{});\n  return (double)sqrtf(ux * ux + uy * uy + uz * uz);\n}",
+                 "  __builtin_amdgcn_s_setprio(2);\n  fix_store_all<SW>(f, a.dst, c, ad, (t & kWallAdj) ? links : 0u, AllQ{});\n  return (double)sqrtf(ux * ux + uy * uy + uz * uz);\n}")],
+    # the 4-cell group lists (C4 x4's y rows) with the pipe's priority flips
+    "g_prio": [("lbm_kernels.hip", "  constexpr bool kPrio = SW && !GROUPS;", "  constexpr bool kPrio = SW;")],
     # the pull-phase priority for the cavity's x-row chunk waves too
     "prio_all": [("lbm_kernels.hip", "  constexpr bool kPrio = SW && !GROUPS;", "  constexpr bool kPrio = !GROUPS;")],
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
