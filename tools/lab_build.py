@@ -151,6 +151,10 @@ PATCHES = {
                  "  __builtin_amdgcn_s_setprio(2);\n  fix_store_all<SW>(f, a.dst, c, ad, (t & kWallAdj) ? links : 0u, AllQ{});\n  return (double)sqrtf(ux * ux + uy * uy + uz * uz);\n}")],
     # the 4-cell group lists (C4 x4's y rows) with the pipe's priority flips
     "g_prio": [("lbm_kernels.hip", "  constexpr bool kPrio = SW && !GROUPS;", "  constexpr bool kPrio = SW;")],
+    # the cavity's x-row chunk waves: stores at raised priority / pulls and stores
+    "box_prio_st": [("lbm_kernels.hip", "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);  // the stores, too",
+                     "  if constexpr (kPrio || BOX) __builtin_amdgcn_s_setprio(2);  // the stores, too")],
+    "box_prio_all": [("lbm_kernels.hip", "  constexpr bool kPrio = SW;", "  constexpr bool kPrio = SW || BOX;")],
     # the pull-phase priority for the cavity's x-row chunk waves too
     "prio_all": [("lbm_kernels.hip", "  constexpr bool kPrio = SW && !GROUPS;", "  constexpr bool kPrio = !GROUPS;")],
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
