@@ -155,6 +155,9 @@ PATCHES = {
     "box_prio_st": [("lbm_kernels.hip", "  if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);  // the stores, too",
                      "  if constexpr (kPrio || BOX) __builtin_amdgcn_s_setprio(2);  // the stores, too")],
     "box_prio_all": [("lbm_kernels.hip", "  constexpr bool kPrio = SW;", "  constexpr bool kPrio = SW || BOX;")],
+    # NEE blocks' threads at raised priority for their whole (latency-bound, scattered) work
+    "nee_prio": [("lbm_kernels.hip", "__device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {\n",
+                  "__device__ __forceinline__ double nee_cell(const MainArgs& a, int i) {\n  __builtin_amdgcn_s_setprio(3);\n")],
     # the pull-phase priority for the cavity's x-row chunk waves too
     "prio_all": [("lbm_kernels.hip", "  constexpr bool kPrio = SW && !GROUPS;", "  constexpr bool kPrio = !GROUPS;")],
     "c1_wg256": [("lbm_kernels.hpp", "constexpr int kBlock1c = 128;", "constexpr int kBlock1c = 256;")],
