@@ -212,8 +212,8 @@ typedef enum {
                                    into its pulls (chunk lists of the dense box with at most 8 such
                                    cells per chunk; otherwise as 3) */
   LBM_TUNE_XCD_RUN = 13,        /* order of the step kernel's chunk workgroups over the 8 XCDs: 0
-                                   (default) runs of four (L = 3) for 4-cell chunk lists whose rows
-                                   run along y (the pipe) and for compact one-cell
+                                   (default) runs of eight (L = 4) for 4-cell chunk lists whose rows
+                                   run along y (the pipe), runs of four (L = 3) for compact one-cell
                                    ranges of several rounds of waves (vessel trees), one contiguous
                                    eighth of the chunks per XCD elsewhere; L = 1..16 runs of 2^(L-1) workgroups, XCD x taking
                                    runs x, x + 8, x + 16, ...; 17 one eighth per XCD everywhere */

@@ -429,14 +429,16 @@ int run_range(lbm_ctx* c, Range& r, int srcbuf, hipStream_t st, const FusedRed* 
   // rocprof in round 5, where LDC 256^3 and 512^3 run 9% / 4% slower that way
   // (profiles/r05p_c3_posts_xcd_rocprof.log, r05_xcd_run_ab.log); with the NEE blocks in the
   // launch (round 6) runs of four beat runs of one by ~0.8 us, 170.4-171.0 vs 171.1-172.8
-  // (r06m_c3_xcd_runs_ab.log, r06o_c3_xcd_runs_ab.log); runs of four blocks for compact one-cell ranges of several rounds of
+  // (r06m_c3_xcd_runs_ab.log, r06o_c3_xcd_runs_ab.log), and with the wave-priority flips runs of
+  // eight beat four, 167.9-168.6 vs 168.9-170.3 us (L = 4; r06zw_c3_xcd_runs_prio_ab.log,
+  // r06zx_...); runs of four blocks for compact one-cell ranges of several rounds of
   // waves -- the coronary tree: 31.1 -> 29.8 us, where one-round C4 runs slower interleaved
   // (r05_c1_xcd_ab.log, r05z_coronary_xcd_ab.log); one contiguous eighth per XCD elsewhere; 17:
   // eighths everywhere.  Not for grid-stride ranges: their waves take work by XCD (b & 7) and
   // round (b >> 3) whatever the order, so a run length would only move their partial slots
   a.xcd_run = (c->xcd_run == 17 || r.stride)                 ? 0
               : c->xcd_run > 0                               ? c->xcd_run
-              : (c->L.swap && !r.quarter && !r.groups)       ? 3
+              : (c->L.swap && !r.quarter && !r.groups)       ? 4
               : (c->compact && r.quarter && !r.one_round)    ? 3
                                                              : 0;
   a.lane_masks = r.quarter ? nullptr : r.lane_masks;

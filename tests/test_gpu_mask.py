@@ -210,7 +210,7 @@ def test_grid_stride_bitwise(gpu, knob, case):
 @pytest.mark.parametrize("lattice", ["pipe_y", "pipe_y_stride", "ldc", "coronary"])
 def test_xcd_run_bitwise(gpu, knob, lattice):
     """LBM_TUNE_XCD_RUN changes only which XCD takes which chunk workgroup: a pipe with rows along
-    y (round robin by default), a cavity (one eighth per XCD by default) and the coronary tree
+    y (runs of eight by default), a cavity (one eighth per XCD by default) and the coronary tree
     (compact one-cell waves, runs of four by default) under both orders and runs of 16 workgroups
     step bit for bit alike, residual histories included (each partial slot sums the same chunks
     whatever the order).  The pipe's grid-stride loop (LBM_TUNE_GRID_STRIDE 2), whose waves take
